@@ -1,0 +1,209 @@
+/*
+ * vissm.h -- C ABI of libvissm.so, the MI355X (gfx950) kernels of the
+ * neural-moving-average variational-inference ELBO step.
+ *
+ * The reference (mehrnazmo/VIforSSMs) is TensorFlow-1.8 Python: it has no FFI.
+ * Every entry point below replaces a group of TF ops that the reference builds
+ * inside VI_SSM.build_flow() and runs each step through sess.run (AR.py:300-301);
+ * the reference interface each one replaces is cited next to it.  The Python
+ * host (viforssms_amd/, loaded through ctypes) mirrors the reference's
+ * Python API on top of these calls: VI_SSM / Flow_Stack / IAF (AR.py:24-362,
+ * lotka_volterra_partial.py, SV_dense.py, fitz_nag_NVP.py) and
+ * optimisers.adamax.AdamaxOptimizer (optimisers/adamax.py:11-61).
+ *
+ * Conventions
+ *   - every buffer is a caller-owned DEVICE pointer (fp32 unless stated);
+ *     layouts are row-major with the TF variable layouts for weights
+ *     (dense [in][out], conv1d [k][C_in][C_out]).
+ *   - every call takes the HIP stream to launch on (hipStream_t passed as
+ *     void*); there is no implicit device synchronisation, no hipSetDevice and
+ *     no allocation on the call path: scratch comes from a caller workspace
+ *     sized by the matching *_workspace_size() query.
+ *   - return value 0 = OK, negative = error (VISSM_E*); vissm_last_error()
+ *     returns a thread-local message for the last failing call.  Nothing
+ *     throws across the ABI and nothing exits.
+ *   - reductions are fixed-order (partial slabs + ordered tree), so results
+ *     are bitwise reproducible run to run; no float atomics.
+ */
+#ifndef VISSM_H
+#define VISSM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VISSM_OK 0
+#define VISSM_EINVAL (-1)   /* bad shape / argument */
+#define VISSM_ELAUNCH (-2)  /* HIP launch or runtime failure */
+#define VISSM_EWORKSPACE (-3)
+
+#define VISSM_PREC_FP32 0     /* exact fp32 arithmetic */
+#define VISSM_PREC_BF16 1     /* bf16 MFMA operands, fp32 accumulation */
+#define VISSM_PREC_BF16X3 2   /* split-bf16 (hi/lo) MFMA operands: ~fp32 products */
+
+const char* vissm_last_error(void);
+int vissm_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Base noise: init_dist.slp (AR.py:24-35; lotka_volterra_partial.py:25-36).
+ * eps[b][j] ~ N(0,1) from counter-based Philox4x32-10 keyed by (seed, offset+b),
+ * base_lp[b] = sum_{j >= L - n_last} log N(eps[b][j]; 0, 1).
+ * ------------------------------------------------------------------------- */
+int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp,
+                      int32_t B, int32_t L, int32_t n_last, void* stream);
+
+/* base_lp only, for caller-supplied eps (parity mode). */
+int vissm_base_logprob(const float* eps, float* base_lp, int32_t B, int32_t L,
+                       int32_t n_last, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * One IAF flow of the neural-MA sampler: IAF._create_flow + IAF.slp
+ * (AR.py:50-89; lotka_volterra_partial.py:68-108 stride-2/BN variant;
+ *  SV_dense.py:50-89; fitz_nag_NVP.py:68-109) with the window-shared part of
+ * the first conv (feature branch, conv over features, conv bias) and the theta
+ * branch precomputed by the caller:
+ *
+ *   a0[b,m,:] = C[win[b], m, :] + theta_term[b, :] + sum_j u[b, s*m + j] * w_eps[j, :]
+ *   x_0 = elu(a0);  x_{l+1} = bn_l(elu(x_l W_l + b_l))     (l < n_hidden)
+ *   (mu, r) = x_nh W_head + b_head;  sigma = softplus(r) + 1e-10
+ *   stride 1: u_next[t] = u[t+k] * sigma[t] + mu[t]
+ *   stride 2: u_next[2m] = u[2m+k];  u_next[2m+1] = u[2m+1+k] * sigma[m] + mu[m]
+ *   logsig[b] = sum of log sigma over the last n_logsig outputs.
+ * swap_out != 0 writes u_next with adjacent pairs swapped (the Permute flow of
+ * the 2-D models, lotka_volterra_partial.py:137-159, fused into the store).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t B;          /* samples (reference p) */
+  int32_t L;          /* input length per sample; output length is L - k */
+  int32_t k;          /* kernel_len, 1..64 */
+  int32_t H;          /* network_dims[i], 1..64 (all equal) */
+  int32_t n_hidden;   /* len(network_dims) - 2, 0..4 */
+  int32_t bn;         /* batch_normalization(training=False) after each hidden ELU */
+  int32_t stride2;    /* 2-D interleaved head (stride 2, (0,1) interleave) */
+  int32_t swap_out;   /* fuse the pair-swap permutation into the output store */
+  int32_t n_logsig;   /* trailing outputs counted in log q: M (1-D) or 2M (2-D) */
+  int32_t n_win;      /* windows in C (1 when every sample shares one window) */
+  int32_t precision;  /* VISSM_PREC_* */
+  int32_t reserved;
+} VissmFlowDesc;
+
+typedef struct {
+  const float* w_eps;   /* [k][H]      conv1d kernel, input channel 0 (the sample) */
+  const float* w_hid;   /* [n_hidden][H][H] conv1d k=1 kernels */
+  const float* b_hid;   /* [n_hidden][H] */
+  const float* bn_g;    /* [n_hidden][H] or NULL (bn == 0) */
+  const float* bn_b;    /* [n_hidden][H] or NULL */
+  const float* w_head;  /* [H][2]  (col 0 = mu, col 1 = sigma pre-softplus) */
+  const float* b_head;  /* [2] */
+} VissmFlowParams;
+
+typedef struct {        /* outputs of the backward: written, not accumulated */
+  float* w_eps; float* w_hid; float* b_hid; float* bn_g; float* bn_b;
+  float* w_head; float* b_head;
+} VissmFlowGrads;
+
+/* C is [n_win][Lh][H] with Lh = (L-k) (stride 1) or (L-k)/2 (stride 2);
+ * win is [B] int32 window index per sample (NULL = all 0). */
+size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward);
+
+int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w,
+                   const float* u, const float* C, const int32_t* win,
+                   const float* theta_term, float* u_next, float* logsig,
+                   void* workspace, size_t ws_bytes, void* stream);
+
+/* Backward of vissm_flow_fwd for a scalar loss.  du_next = dLoss/du_next (in
+ * the stored, possibly swapped layout), dlogsig[b] = dLoss/dlogsig[b].
+ * Writes du [B][L], dC [n_win][Lh][H], dtheta_term [B][H] and the weight
+ * gradients. */
+int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w,
+                   const float* u, const float* C, const int32_t* win,
+                   const float* theta_term, const float* du_next,
+                   const float* dlogsig, float* du, float* dC,
+                   float* dtheta_term, const VissmFlowGrads* g,
+                   void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * ELBO log-densities over a path, one model per id:
+ *   AR  : VI_SSM._ELBO obs + AR(1) terms (AR.py:168-176)
+ *   LV  : softplus transform + ILDJ (lotka_volterra_partial.py:290-297),
+ *         obs N(.,1) and Cholesky EM density (lotka_volterra_partial.py:234-261)
+ *   SV  : dim-one concat + mask/shift (SV_dense.py:245-246), diag EM density (SV_dense.py:203-223)
+ *   FHN : obs N(.,0.1) and diag EM density (fitz_nag_NVP.py:232-255)
+ * z is the flow output [B][D*(M+1)] (2-D models interleaved t-major).
+ * Outputs per sample: sde[b], obs[b] (0 for SV) and extra[b] (LV: ILDJ, else 0).
+ * ------------------------------------------------------------------------- */
+#define VISSM_MODEL_AR 0
+#define VISSM_MODEL_LV 1
+#define VISSM_MODEL_SV 2
+#define VISSM_MODEL_FHN 3
+
+typedef struct {
+  int32_t model;
+  int32_t B;
+  int32_t M;          /* transitions per path (reference batch_dims) */
+  int32_t n_win;
+  float dt;           /* Euler-Maruyama step (LV/SV/FHN) */
+  float obs_std;      /* AR observation sd */
+} VissmElboDesc;
+
+typedef struct {
+  const int32_t* win;     /* [B] or NULL */
+  const float* obs;       /* [n_win][D][M] observation window (AR: [n_win][M]) */
+  const float* obs_bin;   /* [n_win][D][M] observation mask */
+  const float* mask;      /* LV [n_win][2][M+1]; SV [n_win][M+1]; else NULL */
+  const float* shift;     /* same shape as mask */
+  const float* dim_one;   /* SV observed coordinate [n_win][M+1]; else NULL */
+} VissmElboData;
+
+int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data,
+                   const float* z, const float* theta, float* sde, float* obs,
+                   float* extra, void* stream);
+
+/* dLoss/d(sde, obs, extra) per sample -> dz [B][D*(M+1)], dtheta [B][P_theta]. */
+int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data,
+                   const float* z, const float* theta, const float* g_sde,
+                   const float* g_obs, const float* g_extra, float* dz,
+                   float* dtheta, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Global-norm clip + Adamax over one flat parameter buffer:
+ * tf.global_norm / tf.clip_by_global_norm (AR.py:230-232) followed by
+ * AdamaxOptimizer._apply_dense (optimisers/adamax.py:42-58):
+ *   g <- g * clip * min(1/||g||, 1/clip)   (NaN when ||g|| is not finite)
+ *   v <- beta1 v + (1-beta1) g ;  m <- max(beta2 m + eps, |g|) ;  p <- p - lr v/m
+ * clip <= 0 disables clipping.  gnorm_out (device, 1 float, may be NULL)
+ * receives ||g|| before clipping.
+ * ------------------------------------------------------------------------- */
+size_t vissm_adamax_workspace_size(int64_t n);
+int vissm_adamax_step(float* params, const float* grads, float* v, float* m,
+                      int64_t n, float lr, float beta1, float beta2, float eps,
+                      float clip, float* gnorm_out, void* workspace,
+                      size_t ws_bytes, void* stream);
+
+/* Sum of squares of a flat buffer (fixed-order), result to out[0] (device float). */
+int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace,
+                 size_t ws_bytes, void* stream);
+
+/* out[c] = sum_r slab[r][c] for r = 0..R-1 in fixed order (deterministic reduce). */
+int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Opt-in kernel timing (for bench.py's live roofline): when enabled, the flow
+ * entry points bracket their main kernel with hipEvents on the launch stream.
+ * kind: VISSM_PROF_FLOW_FWD / VISSM_PROF_FLOW_BWD.  read() synchronises the
+ * recorded events and returns the summed milliseconds and the launch count.
+ * ------------------------------------------------------------------------- */
+#define VISSM_PROF_FLOW_FWD 0
+#define VISSM_PROF_FLOW_BWD 1
+void vissm_profile_enable(int32_t on);
+int vissm_profile_read(int32_t kind, double* total_ms, int64_t* count);
+void vissm_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VISSM_H */

@@ -1,0 +1,162 @@
+"""Parity harness: run one ELBO evaluation + gradient through the product (libvissm on the GPU)
+and through the CPU oracle (float64) on identical injected inputs, and report the errors.
+
+Used by tests/test_gpu_parity.py and __graft_entry__.smoke()."""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from oracle import nma_oracle as O  # noqa: E402
+from oracle import bridge  # noqa: E402
+
+
+def _ar_data(T: int, seed: int, impute: int = 1):
+    from viforssms_amd.data import data_gen
+    st = np.random.get_state()
+    np.random.seed(seed)
+    obs, ob, tt = data_gen(T, impute, 10.0, np.array([5.0, 0.5, 3.0]), 1.0, write=False)
+    np.random.set_state(st)
+    return obs.astype(np.float32), ob.astype(np.float32), tt.astype(np.float32)
+
+
+def build_model(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
+                device: str, T: Optional[int] = None, precision: int = 0, seed: int = 3):
+    """A small model of the given family with a random (non-trivial) parameter draw."""
+    from viforssms_amd import _lib
+    from viforssms_amd.vi_ssm import ThetaSpec
+    rng = np.random.default_rng(seed)
+    nd = [H] * n_layers
+    if family == "ar":
+        from viforssms_amd.ar import VI_SSM
+        T = T or M
+        obs, ob, tt = _ar_data(T, seed, impute=2)
+        priors = [(0.0, 10.0)] * 3
+        spec = ThetaSpec(5, [list(rng.permutation(3)) for _ in range(4)], 1.5, 0.5, "elu")
+        model = VI_SSM(obs, 1.0, 10.0, spec, priors, T, B, k, M, nd, n_flows, fw, ob, tt, device=device,
+                       precision=precision, init_seed=seed)
+    elif family == "lv":
+        from viforssms_amd.lv import VI_SSM, make_theta_spec
+        from viforssms_amd.data import lv_data_gen
+        T = T or M
+        obs, ob, tt, _ = lv_data_gen(T, dt=0.1, obs_every=max(2, M // 4), seed=seed)
+        priors = [(np.log(4.428 / 10), 1e-4), (np.log(0.029 / 10), 1e-4), (np.log(2.957 / 10), 1e-4)]
+        spec = ThetaSpec(4, [list(rng.permutation(3)) for _ in range(3)], 0.0, 1.0, "elu")
+        model = VI_SSM(obs, ob, tt, np.array([100.0, 100.0]), spec, priors, 0.1, T * 0.1, B, k, M, nd, T,
+                       n_flows, fw, device=device, precision=precision, init_seed=seed)
+    elif family == "sv":
+        from viforssms_amd.sv import VI_SSM
+        from viforssms_amd.data import load_sv
+        obs = load_sv()
+        T = T or M
+        obs = obs[: T + 1]
+        priors = [(0.0, 10.0)] * 4
+        spec = ThetaSpec(5, [list(rng.permutation(4)) for _ in range(4)], 0.0, 1.0, "relu")
+        model = VI_SSM(obs, -8.5, spec, priors, 1.0, T, B, k, M, nd, T, n_flows, fw, device=device,
+                       precision=precision, init_seed=seed)
+    elif family == "fhn":
+        from viforssms_amd.fhn import VI_SSM
+        from viforssms_amd.data import fhn_data_gen
+        T = T or M
+        obs, ob, tt, _ = fhn_data_gen(T, dt=0.1, obs_every=max(2, M // 6), seed=seed)
+        priors = [(0.0, 10.0)] * 5
+        spec = ThetaSpec(4, [list(rng.permutation(5)) for _ in range(3)], 0.0, 1.0, "elu")
+        model = VI_SSM(obs, ob, tt, np.array([2.0, 3.0]), spec, priors, 0.1, T * 0.1, B, k, M, nd, T, n_flows,
+                       fw, device=device, precision=precision, init_seed=seed)
+    else:
+        raise ValueError(family)
+    # perturb every variable (biases included) so all gradient paths are exercised
+    vals = model.store.state_numpy()
+    for name, v in vals.items():
+        if name.startswith("theta/"):
+            continue
+        scale = 0.05 if "bias" in name or "beta" in name else 0.0
+        vals[name] = v + scale * rng.standard_normal(v.shape)
+        if "gamma" in name:
+            vals[name] = v + 0.1 * rng.standard_normal(v.shape)
+    for name, v in vals.items():
+        if name.startswith("theta/") and name.endswith("bias"):
+            vals[name] = 0.05 * rng.standard_normal(v.shape)
+    model.store.load_numpy(vals)
+    model.build_flow()
+    return model
+
+
+def _oracle_extra(model, batch, B):
+    inv = (batch.win.cpu().numpy().astype(np.int64) if batch.win is not None else np.zeros(B, dtype=np.int64))
+    hf = batch.host_feeds
+    ex = {}
+    if "obs_bin" in hf and model.mdef.D == 2:
+        ex["bin"] = torch.tensor(hf["obs_bin"][inv], dtype=O.DT)
+    for key in ("mask", "shift", "dim_one"):
+        if key in hf:
+            ex[key] = torch.tensor(hf[key][inv], dtype=O.DT)
+    return ex, inv
+
+
+def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
+                    device: str = "cuda:0", T: Optional[int] = None, starts=None, precision: int = 0,
+                    seed: int = 3) -> Dict:
+    torch.cuda.set_device(torch.device(device))
+    model = build_model(family, B, M, k, n_flows, H, n_layers, fw, device, T=T, precision=precision, seed=seed)
+    md = model.mdef
+    if starts is None:
+        starts = np.zeros(B, dtype=np.int64)
+    starts = np.asarray(starts, dtype=np.int64)
+    batch = model.engine.make_batch(starts)
+    g = torch.Generator().manual_seed(seed + 11)
+    eps = torch.randn(B, md.kernel_ext, generator=g, dtype=torch.float64)
+    x0 = torch.randn(B, md.P_theta, generator=g, dtype=torch.float64) * md.theta_base[1] + md.theta_base[0]
+
+    # ---- product (GPU) ----
+    st = model.store
+    st.zero_grad()
+    out = model.forward(batch, 0, eps=eps.float().to(device).contiguous(), x0_theta=x0.float().to(device))
+    loss = (-out["elbo"]).sum()
+    loss.backward()
+    st.sync_grads()
+    torch.cuda.synchronize()
+    elbo_gpu = out["elbo"].detach().double().cpu().numpy()
+    grads_gpu = {n: st.grad[a:a + s].double().cpu().numpy().reshape(st.tensors[n].shape)
+                 for n, (a, s) in st.offsets.items()}
+
+    # ---- oracle (CPU float64) ----
+    spec = bridge.spec_from_mdef(md, B)
+    params = bridge.oracle_params(st.state_numpy(), spec, model.engine.theta_dist.masks_np)
+    inv_ex, inv = _oracle_extra(model, batch, B)
+    ts = torch.tensor(batch.ts.double().cpu().numpy()[inv if batch.win is not None else np.zeros(B, dtype=int)],
+                      dtype=O.DT)
+    leaves = O.param_leaves(params)
+    for t in leaves:
+        t.requires_grad_(True)
+    o = O.elbo(spec, params, model.engine.perms, x0, eps, ts, inv_ex)
+    (-o["elbo"]).sum().backward()
+    ref_g = bridge.oracle_grads_by_name(params, [t.grad if t.grad is not None else torch.zeros_like(t)
+                                                 for t in leaves], spec)
+    elbo_ref = o["elbo"].detach().numpy()
+
+    elbo_err = float(np.max(np.abs(elbo_gpu - elbo_ref) / np.maximum(np.abs(elbo_ref), 1e-6)))
+    gref = np.concatenate([ref_g[n].ravel() for n in st.names()])
+    ggpu = np.concatenate([grads_gpu[n].ravel() for n in st.names()])
+    gnorm = np.linalg.norm(gref)
+    per = {}
+    for n in st.names():
+        r, q = ref_g[n], grads_gpu[n]
+        per[n] = float(np.linalg.norm(q - r) / (np.linalg.norm(r) + 1e-6 * gnorm + 1e-30))
+    return {
+        "elbo_rel_err": elbo_err,
+        "grad_rel_err": float(np.linalg.norm(ggpu - gref) / (gnorm + 1e-30)),
+        "grad_max_param_err": max(per.values()),
+        "worst_param": max(per, key=per.get),
+        "elbo_ref_mean": float(elbo_ref.mean()),
+        "per_param": per,
+        "finite": bool(np.isfinite(elbo_gpu).all() and np.isfinite(ggpu).all()),
+    }

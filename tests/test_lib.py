@@ -1,0 +1,123 @@
+"""The C-ABI library: it loads without a GPU, exports every symbol include/vissm.h declares, and the
+hand-derived ELBO transition gradients (compiled for the host from the same header the kernels use)
+match the oracle's autograd.  No GPU compute here."""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nma_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vissm.h")
+HOSTCHECK = os.path.join(ROOT, "viforssms_amd", "libvissm_hostcheck.so")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(vissm_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_all_symbols():
+    from viforssms_amd import _lib
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} not bound in _lib.SIGNATURES"
+    assert lib.vissm_version() >= 1
+
+
+def test_library_rejects_bad_shapes_without_gpu():
+    from viforssms_amd import _lib
+    lib = _lib.load()
+    d = _lib.FlowDesc(4, 10, 99, 16, 1, 0, 0, 0, 5, 1, 0, 0)  # k > 64
+    assert lib.vissm_flow_workspace_size(ctypes.byref(d), 0) == 0
+    rc = lib.vissm_normal_base(1, 0, None, None, 2, 0, 0, None)
+    assert rc < 0 and b"bad shape" in lib.vissm_last_error()
+
+
+def _host():
+    lib = ctypes.CDLL(HOSTCHECK)
+    f = lib.vissm_host_trans
+    f.restype = None
+    f.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_float)] * 3 + [ctypes.c_float, ctypes.POINTER(ctypes.c_float)]
+    return lib
+
+
+def _arr(v):
+    a = (ctypes.c_float * len(v))(*[float(x) for x in v])
+    return a
+
+
+def _oracle_trans(model, xh, xt, th, dt):
+    """lp and gradients of one transition from the oracle's density functions (float64 autograd)."""
+    xh_t = torch.tensor(xh, dtype=O.DT, requires_grad=True)
+    xt_t = torch.tensor(xt, dtype=O.DT, requires_grad=True)
+    th_t = torch.tensor(th, dtype=O.DT, requires_grad=True)
+    if model == 0:
+        x = torch.stack([xh_t[0], xt_t[0]]).view(1, 2)
+        lp, _ = O.ar_elbo_terms(x, th_t.view(1, -1), torch.zeros(1, 1, dtype=O.DT), torch.zeros(1, 1, dtype=O.DT), 1.0)
+    else:
+        x = torch.stack([xh_t, xt_t], 1).view(1, 2, 2)
+        if model == 1:
+            lp, _ = O.lv_elbo_terms(x, th_t.view(1, -1), torch.zeros(1, 2, 1, dtype=O.DT),
+                                    torch.zeros(1, 2, 1, dtype=O.DT), dt)
+        elif model == 2:
+            lp = O.sv_elbo_terms(x, th_t.view(1, -1), dt)
+        else:
+            lp, _ = O.fhn_elbo_terms(x, th_t.view(1, -1), torch.zeros(1, 2, 1, dtype=O.DT),
+                                     torch.zeros(1, 2, 1, dtype=O.DT), dt)
+    lp = lp.sum()
+    gh, gt, gth = torch.autograd.grad(lp, [xh_t, xt_t, th_t])
+    return lp.item(), gh.numpy(), gt.numpy(), gth.numpy()
+
+
+CASES = [
+    (0, [10.3], [12.1], [5.0, 0.5, math.log(3.0)], 1.0),
+    (0, [-2.0], [0.7], [0.3, -0.9, -0.4], 1.0),
+    (1, [100.0, 90.0], [103.0, 88.5], [math.log(0.5), math.log(0.0025), math.log(0.3)], 0.1),
+    (1, [20.0, 300.0], [19.0, 305.0], [math.log(0.44), math.log(0.003), math.log(0.29)], 0.1),
+    (2, [3.1, -8.0], [3.3, -7.7], [0.01, -0.6, math.log(0.08), math.log(0.5)], 1.0),
+    (3, [0.4, 1.2], [0.45, 1.3], [math.log(2.0), 1.0, 1.5, math.log(0.5), math.log(0.3)], 0.1),
+    (3, [-1.5, 0.2], [-1.4, 0.1], [0.2, -0.5, 0.7, -1.0, 0.3], 0.1),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_transition_gradients_match_oracle(case):
+    model, xh, xt, th, dt = case
+    lib = _host()
+    out = (ctypes.c_float * 10)()
+    xh2 = list(xh) + [0.0] * (2 - len(xh))
+    xt2 = list(xt) + [0.0] * (2 - len(xt))
+    lib.vissm_host_trans(model, _arr(xh2), _arr(xt2), _arr(list(th) + [0.0] * (5 - len(th))), dt, out)
+    lp, gh, gt, gth = _oracle_trans(model, xh, xt, th, dt)
+    D = len(xh)
+    got = np.array(out[:])
+    scale = max(1.0, abs(lp))
+    assert abs(got[0] - lp) <= 2e-6 * scale
+    gscale = max(1.0, np.abs(np.concatenate([gh, gt, gth])).max())
+    assert np.allclose(got[1:1 + D], gh, atol=3e-5 * gscale, rtol=1e-4)
+    assert np.allclose(got[3:3 + D], gt, atol=3e-5 * gscale, rtol=1e-4)
+    assert np.allclose(got[5:5 + len(th)], gth, atol=3e-5 * gscale, rtol=1e-4)
+
+
+def test_softplus_ildj_matches_oracle():
+    lib = ctypes.CDLL(HOSTCHECK)
+    f = lib.vissm_host_sp_ildj
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_float)]
+    for y in (0.05, 0.7, 3.0, 40.0):
+        g = ctypes.c_float()
+        v = f(y, ctypes.byref(g))
+        yt = torch.tensor(y, dtype=O.DT, requires_grad=True)
+        ref = -torch.log(-torch.expm1(-yt))
+        (gr,) = torch.autograd.grad(ref, [yt])
+        assert abs(v - ref.item()) <= 1e-5 * max(1, abs(ref.item()))
+        assert abs(g.value - gr.item()) <= 1e-4 * max(1, abs(gr.item()))

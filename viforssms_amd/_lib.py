@@ -1,0 +1,120 @@
+"""ctypes binding of libvissm.so (include/vissm.h).
+
+The product path calls the HIP kernels only through this module.  There is no
+CPU or PyTorch fallback: if the library is missing or a call fails, an error is
+raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvissm.so")
+
+VISSM_PREC_FP32 = 0
+VISSM_PREC_BF16 = 1
+VISSM_PREC_BF16X3 = 2
+
+MODEL_AR, MODEL_LV, MODEL_SV, MODEL_FHN = 0, 1, 2, 3
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_f32 = ctypes.c_float
+_size_t = ctypes.c_size_t
+
+
+class FlowDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("B", "L", "k", "H", "n_hidden", "bn", "stride2", "swap_out",
+                                    "n_logsig", "n_win", "precision", "reserved")]
+
+
+class FlowParams(ctypes.Structure):
+    _fields_ = [(n, _c_void_p) for n in ("w_eps", "w_hid", "b_hid", "bn_g", "bn_b", "w_head", "b_head")]
+
+
+class FlowGrads(ctypes.Structure):
+    _fields_ = [(n, _c_void_p) for n in ("w_eps", "w_hid", "b_hid", "bn_g", "bn_b", "w_head", "b_head")]
+
+
+class ElboDesc(ctypes.Structure):
+    _fields_ = [("model", _i32), ("B", _i32), ("M", _i32), ("n_win", _i32), ("dt", _f32), ("obs_std", _f32)]
+
+
+class ElboData(ctypes.Structure):
+    _fields_ = [(n, _c_void_p) for n in ("win", "obs", "obs_bin", "mask", "shift", "dim_one")]
+
+
+# exported symbol -> (restype, argtypes); tests check that every symbol of include/vissm.h is here
+SIGNATURES = {
+    "vissm_last_error": (ctypes.c_char_p, []),
+    "vissm_version": (_i32, []),
+    "vissm_normal_base": (_i32, [_u64, _u64, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
+    "vissm_base_logprob": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
+    "vissm_flow_workspace_size": (_size_t, [ctypes.POINTER(FlowDesc), _i32]),
+    "vissm_flow_fwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "vissm_flow_bwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                              ctypes.POINTER(FlowGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vissm_adamax_workspace_size": (_size_t, [_i64]),
+    "vissm_adamax_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
+                                 _f32, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
+    "vissm_profile_enable": (None, [_i32]),
+    "vissm_profile_read": (_i32, [_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
+    "vissm_profile_reset": (None, []),
+}
+
+PROF_FLOW_FWD, PROF_FLOW_BWD = 0, 1
+
+
+class VissmError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libvissm.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise VissmError(
+            f"libvissm.so not found at {path}; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C viforssms_amd/csrc`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().vissm_last_error()
+        raise VissmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> Optional[int]:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,298 @@
+// ELBO log-density kernels: one 256-thread block per trajectory, fixed-order
+// block reductions (double accumulation).  Streaming: the path z is read once
+// (forward) or once plus its neighbours (backward, which recomputes each
+// transition from both of its endpoints instead of exchanging partials).
+//
+// Reference terms: AR VI_SSM._ELBO (AR.py:168-187); LV Softplus transform and
+// _ELBO (lotka_volterra_partial.py:290-297, 234-270); SV dim-one concat and
+// _ELBO (SV_dense.py:245-246, 203-232); FHN _ELBO (fitz_nag_NVP.py:232-265).
+#include "common.hpp"
+#include "elbo_math.hpp"
+
+namespace vissm {
+namespace elbo {
+
+struct Args {
+  int B, M, n_win;
+  float dt, obs_std;
+  VissmElboData d;
+};
+
+template <int MODEL>
+struct Model;
+
+// x at time t for dimension d and its derivative w.r.t. the stored z entry
+template <>
+struct Model<VISSM_MODEL_AR> {
+  static constexpr int D = 1, P = 3;
+  __device__ static float x(const Args&, const float* zb, int, int t, int, float* dxdz) {
+    *dxdz = 1.f;
+    return zb[t];
+  }
+  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float) {
+    return em::ar_trans(xh[0], xt[0], th);
+  }
+  __device__ static int zidx(int t, int) { return t; }
+};
+
+template <>
+struct Model<VISSM_MODEL_LV> {
+  static constexpr int D = 2, P = 3;
+  __device__ static float x(const Args& a, const float* zb, int w, int t, int d, float* dxdz) {
+    const float zz = zb[2 * t + d];
+    const size_t mi = (static_cast<size_t>(w) * 2 + d) * (a.M + 1) + t;
+    const float mk = a.d.mask[mi];
+    *dxdz = mk * em::sigmoid_h(zz);
+    return em::softplus_h(zz) * mk + a.d.shift[mi];
+  }
+  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
+    return em::lv_trans(xh, xt, th, dt);
+  }
+  __device__ static int zidx(int t, int d) { return 2 * t + d; }
+};
+
+template <>
+struct Model<VISSM_MODEL_SV> {
+  static constexpr int D = 2, P = 4;
+  __device__ static float x(const Args& a, const float* zb, int w, int t, int d, float* dxdz) {
+    const size_t mi = static_cast<size_t>(w) * (a.M + 1) + t;
+    if (d == 0) {
+      *dxdz = 0.f;
+      return a.d.dim_one[mi];
+    }
+    const float mk = a.d.mask[mi];
+    *dxdz = mk;
+    return zb[t] * mk + a.d.shift[mi];
+  }
+  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
+    return em::sv_trans(xh, xt, th, dt);
+  }
+  __device__ static int zidx(int t, int) { return t; }
+};
+
+template <>
+struct Model<VISSM_MODEL_FHN> {
+  static constexpr int D = 2, P = 5;
+  __device__ static float x(const Args&, const float* zb, int, int t, int d, float* dxdz) {
+    *dxdz = 1.f;
+    return zb[2 * t + d];
+  }
+  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
+    return em::fhn_trans(xh, xt, th, dt);
+  }
+  __device__ static int zidx(int t, int d) { return 2 * t + d; }
+};
+
+// number of stored z entries per sample
+template <int MODEL>
+__device__ __forceinline__ int zlen(const Args& a) {
+  return (MODEL == VISSM_MODEL_LV || MODEL == VISSM_MODEL_FHN) ? 2 * (a.M + 1) : (a.M + 1);
+}
+
+template <int MODEL>
+__device__ __forceinline__ float obs_sd(const Args& a) {
+  return MODEL == VISSM_MODEL_AR ? a.obs_std : (MODEL == VISSM_MODEL_FHN ? 0.1f : 1.f);
+}
+template <int MODEL>
+__device__ __forceinline__ constexpr bool has_obs() { return MODEL != VISSM_MODEL_SV; }
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void elbo_fwd_kernel(Args a, const float* __restrict__ z,
+                                                       const float* __restrict__ theta, float* __restrict__ sde,
+                                                       float* __restrict__ obs, float* __restrict__ extra) {
+  using Mdl = Model<MODEL>;
+  constexpr int D = Mdl::D, P = Mdl::P;
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const int w = a.d.win ? a.d.win[b] : 0;
+  const float* zb = z + static_cast<size_t>(b) * zlen<MODEL>(a);
+  float th[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < P; ++i) th[i] = theta[static_cast<size_t>(b) * P + i];
+  const float osd = obs_sd<MODEL>(a);
+  double s_sde = 0.0, s_obs = 0.0, s_ex = 0.0;
+  for (int t = threadIdx.x; t < a.M; t += blockDim.x) {
+    float xh[2], xt[2], dd;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      xh[d] = Mdl::x(a, zb, w, t, d, &dd);
+      xt[d] = Mdl::x(a, zb, w, t + 1, d, &dd);
+    }
+    s_sde += Mdl::trans(xh, xt, th, a.dt).lp;
+    if (has_obs<MODEL>()) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const size_t oi = (static_cast<size_t>(w) * D + d) * a.M + t;
+        float gx;
+        s_obs += em::obs_term(xt[d], a.d.obs[oi], a.d.obs_bin[oi], osd, &gx);
+      }
+    }
+    if (MODEL == VISSM_MODEL_LV) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        float gy;
+        s_ex += em::sp_ildj(xt[d], &gy);
+      }
+    }
+  }
+  const double r0 = block_sum(s_sde, red);
+  const double r1 = block_sum(s_obs, red);
+  const double r2 = block_sum(s_ex, red);
+  if (threadIdx.x == 0) {
+    sde[b] = static_cast<float>(r0);
+    if (obs) obs[b] = static_cast<float>(r1);
+    if (extra) extra[b] = static_cast<float>(r2);
+  }
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __restrict__ z,
+                                                       const float* __restrict__ theta,
+                                                       const float* __restrict__ g_sde,
+                                                       const float* __restrict__ g_obs,
+                                                       const float* __restrict__ g_ex, float* __restrict__ dz,
+                                                       float* __restrict__ dtheta) {
+  using Mdl = Model<MODEL>;
+  constexpr int D = Mdl::D, P = Mdl::P;
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const int w = a.d.win ? a.d.win[b] : 0;
+  const float* zb = z + static_cast<size_t>(b) * zlen<MODEL>(a);
+  float* dzb = dz + static_cast<size_t>(b) * zlen<MODEL>(a);
+  float th[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < P; ++i) th[i] = theta[static_cast<size_t>(b) * P + i];
+  const float gs = g_sde ? g_sde[b] : 0.f;
+  const float go = (has_obs<MODEL>() && g_obs) ? g_obs[b] : 0.f;
+  const float ge = (MODEL == VISSM_MODEL_LV && g_ex) ? g_ex[b] : 0.f;
+  const float osd = obs_sd<MODEL>(a);
+  double acc[5] = {0, 0, 0, 0, 0};
+  for (int t = threadIdx.x; t <= a.M; t += blockDim.x) {
+    float xc[2], jac[2], xo[2], dd;
+#pragma unroll
+    for (int d = 0; d < D; ++d) xc[d] = Mdl::x(a, zb, w, t, d, &jac[d]);
+    float gx[2] = {0.f, 0.f};
+    if (t < a.M) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[d] = Mdl::x(a, zb, w, t + 1, d, &dd);
+      const em::TG r = Mdl::trans(xc, xo, th, a.dt);
+#pragma unroll
+      for (int d = 0; d < D; ++d) gx[d] += gs * r.gh[d];
+#pragma unroll
+      for (int i = 0; i < P; ++i) acc[i] += static_cast<double>(gs) * r.gth[i];
+    }
+    if (t >= 1) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[d] = Mdl::x(a, zb, w, t - 1, d, &dd);
+      const em::TG r = Mdl::trans(xo, xc, th, a.dt);
+#pragma unroll
+      for (int d = 0; d < D; ++d) gx[d] += gs * r.gt[d];
+      if (has_obs<MODEL>()) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const size_t oi = (static_cast<size_t>(w) * D + d) * a.M + (t - 1);
+          float g;
+          em::obs_term(xc[d], a.d.obs[oi], a.d.obs_bin[oi], osd, &g);
+          gx[d] += go * g;
+        }
+      }
+      if (MODEL == VISSM_MODEL_LV) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          float g;
+          em::sp_ildj(xc[d], &g);
+          gx[d] += ge * g;
+        }
+      }
+    }
+    if (MODEL == VISSM_MODEL_SV) {
+      dzb[t] = gx[1] * jac[1];
+    } else {
+#pragma unroll
+      for (int d = 0; d < D; ++d) dzb[Mdl::zidx(t, d)] = gx[d] * jac[d];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const double s = block_sum(acc[i], red);
+    if (threadIdx.x == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(s);
+  }
+}
+
+static int check(const VissmElboDesc* d, const VissmElboData* data) {
+  VISSM_CHECK_ARG(d && data, "elbo: null desc/data");
+  VISSM_CHECK_ARG(d->B >= 0 && d->M >= 1 && d->n_win >= 1, "elbo: bad shape B=%d M=%d n_win=%d", d->B, d->M,
+                  d->n_win);
+  VISSM_CHECK_ARG(d->n_win == 1 || data->win, "elbo: n_win > 1 needs win[]");
+  switch (d->model) {
+    case VISSM_MODEL_AR:
+    case VISSM_MODEL_FHN:
+      VISSM_CHECK_ARG(data->obs && data->obs_bin, "elbo: model needs obs/obs_bin");
+      break;
+    case VISSM_MODEL_LV:
+      VISSM_CHECK_ARG(data->obs && data->obs_bin && data->mask && data->shift, "elbo: LV needs obs/bin/mask/shift");
+      break;
+    case VISSM_MODEL_SV:
+      VISSM_CHECK_ARG(data->mask && data->shift && data->dim_one, "elbo: SV needs mask/shift/dim_one");
+      break;
+    default:
+      VISSM_CHECK_ARG(false, "elbo: unknown model %d", d->model);
+  }
+  return VISSM_OK;
+}
+
+static Args make(const VissmElboDesc* d, const VissmElboData* data) {
+  Args a;
+  a.B = d->B; a.M = d->M; a.n_win = d->n_win; a.dt = d->dt; a.obs_std = d->obs_std; a.d = *data;
+  if (d->n_win == 1) a.d.win = nullptr;
+  return a;
+}
+
+}  // namespace elbo
+}  // namespace vissm
+
+using namespace vissm;
+using namespace vissm::elbo;
+
+extern "C" {
+
+int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta, float* sde,
+                   float* obs, float* extra, void* stream) {
+  int rc = check(d, data);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(z && theta && sde, "elbo_fwd: null pointer");
+  if (d->B == 0) return VISSM_OK;
+  Args a = make(d, data);
+  hipStream_t st = as_stream(stream);
+  dim3 grid(d->B), blk(256);
+  switch (d->model) {
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_AR>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    default: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+  }
+  VISSM_CHECK_LAUNCH("elbo_fwd");
+  return VISSM_OK;
+}
+
+int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta,
+                   const float* g_sde, const float* g_obs, const float* g_extra, float* dz, float* dtheta,
+                   void* stream) {
+  int rc = check(d, data);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(z && theta && dz && dtheta, "elbo_bwd: null pointer");
+  if (d->B == 0) return VISSM_OK;
+  Args a = make(d, data);
+  hipStream_t st = as_stream(stream);
+  dim3 grid(d->B), blk(256);
+  switch (d->model) {
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_AR>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    default: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+  }
+  VISSM_CHECK_LAUNCH("elbo_bwd");
+  return VISSM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,28 @@
+// Host (CPU) build of elbo_math.hpp so the CPU test-suite can check the
+// hand-derived transition gradients against the oracle's autograd without a GPU.
+// Not part of the product path: libvissm_hostcheck.so is loaded only by tests/.
+#include "elbo_math.hpp"
+
+extern "C" {
+
+// out = [lp, gh0, gh1, gt0, gt1, gth0..gth4]
+void vissm_host_trans(int model, const float* xh, const float* xt, const float* th, float dt, float* out) {
+  using namespace vissm::em;
+  TG r;
+  switch (model) {
+    case 0: r = ar_trans(xh[0], xt[0], th); break;
+    case 1: r = lv_trans(xh, xt, th, dt); break;
+    case 2: r = sv_trans(xh, xt, th, dt); break;
+    default: r = fhn_trans(xh, xt, th, dt); break;
+  }
+  out[0] = r.lp;
+  out[1] = r.gh[0]; out[2] = r.gh[1];
+  out[3] = r.gt[0]; out[4] = r.gt[1];
+  for (int i = 0; i < 5; ++i) out[5 + i] = r.gth[i];
+}
+
+float vissm_host_sp_ildj(float y, float* gy) { return vissm::em::sp_ildj(y, gy); }
+
+float vissm_host_obs(float x, float y, float bin, float sd, float* gx) { return vissm::em::obs_term(x, y, bin, sd, gx); }
+
+}

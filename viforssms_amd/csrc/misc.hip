@@ -1,0 +1,285 @@
+// libvissm: error state, base noise (init_dist), deterministic row reduction,
+// global-norm clip + Adamax (optimisers/adamax.py:42-58, AR.py:230-232).
+#include "common.hpp"
+
+#include <cstdarg>
+#include <cmath>
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+namespace vissm {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ---------------------------------------------------------------------------
+// base noise + base log-prob.  One block per sample row; Philox counter =
+// (column group, row + offset) so the stream is independent of the launch
+// geometry and of how rows are sharded across ranks.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_t offset, float* __restrict__ eps,
+                                                          float* __restrict__ base_lp, int L, int n_last) {
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const uint64_t row = offset + static_cast<uint64_t>(b);
+  const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  float* out = eps + static_cast<size_t>(b) * L;
+  double acc = 0.0;
+  for (int g = threadIdx.x; g * 4 < L; g += blockDim.x) {
+    u4 c{static_cast<uint32_t>(g), 0u, static_cast<uint32_t>(row), static_cast<uint32_t>(row >> 32)};
+    u4 r = philox4x32_10(c, k0, k1);
+    float r1 = sqrtf(-2.f * logf(u01(r.x))), r2 = sqrtf(-2.f * logf(u01(r.z)));
+    float a1 = 6.283185307179586f * u01(r.y), a2 = 6.283185307179586f * u01(r.w);
+    float v[4] = {r1 * cosf(a1), r1 * sinf(a1), r2 * cosf(a2), r2 * sinf(a2)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int j = g * 4 + q;
+      if (j < L) {
+        out[j] = v[q];
+        if (j >= L - n_last) acc += -0.5 * static_cast<double>(v[q]) * v[q];
+      }
+    }
+  }
+  double s = block_sum(acc, red);
+  if (threadIdx.x == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
+}
+
+__global__ __launch_bounds__(256) void base_logprob_kernel(const float* __restrict__ eps, float* __restrict__ base_lp,
+                                                           int L, int n_last) {
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const float* row = eps + static_cast<size_t>(b) * L;
+  double acc = 0.0;
+  for (int j = L - n_last + threadIdx.x; j < L; j += blockDim.x) acc += -0.5 * static_cast<double>(row[j]) * row[j];
+  double s = block_sum(acc, red);
+  if (threadIdx.x == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
+}
+
+// ---------------------------------------------------------------------------
+// out[c] = sum_r slab[r][c], fixed order.  Columns across threads (coalesced),
+// rows split in chunks of RCH across blockIdx.y then summed in order by a second pass.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          int64_t R, int64_t N, int64_t rows_per_part) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
+  const int64_t r1 = min(R, r0 + rows_per_part);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += slab[r * N + c];
+  out[static_cast<int64_t>(blockIdx.y) * N + c] = s;
+}
+
+int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipStream_t st) {
+  if (R <= 0 || N <= 0) return VISSM_OK;
+  // single pass: rows summed sequentially per column (deterministic)
+  dim3 grid(static_cast<unsigned>((N + 255) / 256), 1);
+  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(256), 0, st, slab, out, R, N, R);
+  VISSM_CHECK_LAUNCH("reduce_rows");
+  return VISSM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// global norm + clip + Adamax
+// ---------------------------------------------------------------------------
+constexpr int kNormBlocks = 1024;
+
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                             double* __restrict__ part) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * 4;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n && ((reinterpret_cast<uintptr_t>(x + i) & 15) == 0)) {
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      acc += static_cast<double>(v.x) * v.x + static_cast<double>(v.y) * v.y + static_cast<double>(v.z) * v.z +
+             static_cast<double>(v.w) * v.w;
+    } else {
+      for (int64_t j = i; j < min(n, i + 4); ++j) acc += static_cast<double>(x[j]) * x[j];
+    }
+  }
+  double s = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void sqnorm_final_kernel(const double* __restrict__ part, int np,
+                                                            float* __restrict__ sq_out, float* __restrict__ norm_out,
+                                                            float* __restrict__ scale_out, float clip) {
+  __shared__ double red[16];
+  double v = threadIdx.x < np ? part[threadIdx.x] : 0.0;
+  double s = block_sum(v, red);
+  if (threadIdx.x == 0) {
+    double nrm = sqrt(s);
+    if (sq_out) *sq_out = static_cast<float>(s);
+    if (norm_out) *norm_out = static_cast<float>(nrm);
+    if (scale_out) {
+      // tf.clip_by_global_norm: clip * min(1/norm, 1/clip); non-finite norm -> NaN
+      float sc;
+      if (clip <= 0.f) sc = 1.f;
+      else if (!isfinite(nrm)) sc = NAN;
+      else sc = static_cast<float>(static_cast<double>(clip) * fmin(1.0 / nrm, 1.0 / static_cast<double>(clip)));
+      *scale_out = sc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void adamax_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                     float* __restrict__ v, float* __restrict__ m, int64_t n,
+                                                     const float* __restrict__ scale_ptr, float lr, float b1,
+                                                     float b2, float eps) {
+  const float sc = *scale_ptr;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gi = g[i] * sc;
+    float vi = b1 * v[i] + (1.f - b1) * gi;
+    float mi = fmaxf(b2 * m[i] + eps, fabsf(gi));
+    v[i] = vi;
+    m[i] = mi;
+    p[i] = p[i] - lr * (vi / mi);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// opt-in event timing
+// ---------------------------------------------------------------------------
+struct ProfRec {
+  int kind;
+  hipEvent_t a, b;
+};
+static bool g_prof = false;
+static std::mutex g_prof_mu;
+static std::vector<ProfRec> g_prof_recs;
+static thread_local hipEvent_t g_open[2] = {nullptr, nullptr};
+
+bool prof_on() { return g_prof; }
+
+void prof_begin(int kind, hipStream_t st) {
+  if (!g_prof) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, st);
+  g_open[kind & 1] = e;
+}
+
+void prof_end(int kind, hipStream_t st) {
+  if (!g_prof || !g_open[kind & 1]) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, st);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_recs.push_back({kind, g_open[kind & 1], e});
+  g_open[kind & 1] = nullptr;
+}
+
+}  // namespace vissm
+
+using namespace vissm;
+
+extern "C" {
+
+const char* vissm_last_error(void) { return vissm::g_err; }
+int vissm_version(void) { return 1; }
+
+int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp, int32_t B, int32_t L,
+                      int32_t n_last, void* stream) {
+  VISSM_CHECK_ARG(B >= 0 && L > 0 && n_last >= 0 && n_last <= L, "normal_base: bad shape B=%d L=%d n_last=%d", B,
+                  L, n_last);
+  VISSM_CHECK_ARG(eps && base_lp, "normal_base: null pointer");
+  if (B == 0) return VISSM_OK;
+  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, offset, eps, base_lp, L,
+                     n_last);
+  VISSM_CHECK_LAUNCH("normal_base");
+  return VISSM_OK;
+}
+
+int vissm_base_logprob(const float* eps, float* base_lp, int32_t B, int32_t L, int32_t n_last, void* stream) {
+  VISSM_CHECK_ARG(B >= 0 && L > 0 && n_last >= 0 && n_last <= L, "base_logprob: bad shape");
+  VISSM_CHECK_ARG(eps && base_lp, "base_logprob: null pointer");
+  if (B == 0) return VISSM_OK;
+  hipLaunchKernelGGL(base_logprob_kernel, dim3(B), dim3(256), 0, as_stream(stream), eps, base_lp, L, n_last);
+  VISSM_CHECK_LAUNCH("base_logprob");
+  return VISSM_OK;
+}
+
+int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, void* stream) {
+  VISSM_CHECK_ARG(slab && out && R >= 0 && N >= 0, "reduce_rows: bad args");
+  return launch_reduce_rows(slab, out, R, N, as_stream(stream));
+}
+
+size_t vissm_adamax_workspace_size(int64_t n) {
+  (void)n;
+  return align_up(kNormBlocks * sizeof(double)) + align_up(4 * sizeof(float));
+}
+
+static int sqnorm_impl(const float* x, int64_t n, float* sq_out, float* norm_out, float* scale_out, float clip,
+                       void* ws, size_t ws_bytes, hipStream_t st) {
+  VISSM_CHECK_ARG(ws && ws_bytes >= vissm_adamax_workspace_size(n), "workspace too small");
+  double* part = reinterpret_cast<double*>(ws);
+  int nb = static_cast<int>(std::min<int64_t>(kNormBlocks, std::max<int64_t>(1, (n + 1023) / 1024)));
+  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, x, n, part);
+  VISSM_CHECK_LAUNCH("sqnorm_partial");
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(1024), 0, st, part, nb, sq_out, norm_out, scale_out, clip);
+  VISSM_CHECK_LAUNCH("sqnorm_final");
+  return VISSM_OK;
+}
+
+int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace, size_t ws_bytes, void* stream) {
+  VISSM_CHECK_ARG(x && out && n >= 0, "sqnorm: bad args");
+  return sqnorm_impl(x, n, out, nullptr, nullptr, 0.f, workspace, ws_bytes, as_stream(stream));
+}
+
+int vissm_adamax_step(float* params, const float* grads, float* v, float* m, int64_t n, float lr, float beta1,
+                      float beta2, float eps, float clip, float* gnorm_out, void* workspace, size_t ws_bytes,
+                      void* stream) {
+  VISSM_CHECK_ARG(params && grads && v && m && n >= 0, "adamax_step: bad args");
+  hipStream_t st = as_stream(stream);
+  float* scratch = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + align_up(kNormBlocks * sizeof(double)));
+  int rc = sqnorm_impl(grads, n, nullptr, gnorm_out ? gnorm_out : scratch + 1, scratch, clip, workspace, ws_bytes, st);
+  if (rc) return rc;
+  int nb = static_cast<int>(std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)));
+  hipLaunchKernelGGL(adamax_kernel, dim3(nb), dim3(256), 0, st, params, grads, v, m, n, scratch, lr, beta1, beta2,
+                     eps);
+  VISSM_CHECK_LAUNCH("adamax");
+  return VISSM_OK;
+}
+
+void vissm_profile_enable(int32_t on) { vissm::g_prof = on != 0; }
+
+void vissm_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(vissm::g_prof_mu);
+  for (auto& r : vissm::g_prof_recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  vissm::g_prof_recs.clear();
+}
+
+int vissm_profile_read(int32_t kind, double* total_ms, int64_t* count) {
+  VISSM_CHECK_ARG(total_ms && count, "profile_read: null pointer");
+  std::lock_guard<std::mutex> lk(vissm::g_prof_mu);
+  double tot = 0.0;
+  int64_t n = 0;
+  for (auto& r : vissm::g_prof_recs) {
+    if (r.kind != kind) continue;
+    if (hipEventSynchronize(r.b) != hipSuccess) {
+      set_error("profile_read: event sync failed");
+      return VISSM_ELAUNCH;
+    }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    tot += ms;
+    ++n;
+  }
+  *total_ms = tot;
+  *count = n;
+  return VISSM_OK;
+}
+
+}  // extern "C"

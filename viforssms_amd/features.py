@@ -1,0 +1,133 @@
+"""Window / feature assembly (host side, numpy): the padded per-channel arrays each
+reference VI_SSM.__init__ builds once, and the per-step window gather of its train loop.
+
+A ``FeatureTable`` holds the padded channel arrays; ``windows(starts)`` returns the
+``time_feats`` feed [n, kernel_ext, C] for window starts (in reference units:
+``batch_select``), and ``feeds(starts)`` the per-window ELBO feeds.  Only the
+distinct windows of a step are gathered; samples map to them through ``win``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+
+@dataclass
+class FeatureTable:
+    family: str
+    M: int
+    kext: int
+    chans: List[np.ndarray]           # padded channel arrays
+    stride: int                        # 1 (AR/SV) or 2 (LV/FHN: starts are doubled)
+    extra: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    @property
+    def C(self) -> int:
+        return len(self.chans)
+
+    def windows(self, starts) -> np.ndarray:
+        starts = np.asarray(starts, dtype=np.int64)
+        out = np.empty((len(starts), self.kext, self.C), dtype=np.float64)
+        for r, s in enumerate(starts):
+            a = self.stride * int(s)
+            for c, arr in enumerate(self.chans):
+                out[r, :, c] = arr[a:a + self.kext]
+        return out
+
+    def feeds(self, starts, ts: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
+        """Per-window ELBO feeds (obs/obs_bin/mask/shift/dim_one) in the kernel layouts."""
+        starts = np.asarray(starts, dtype=np.int64)
+        ts = self.windows(starts) if ts is None else ts
+        M = self.M
+        n = len(starts)
+        out: Dict[str, np.ndarray] = {}
+        if self.family == "ar":                                   # AR.py:155, AR.py:170
+            out["obs"] = ts[:, -M:, 0]
+            out["obs_bin"] = ts[:, -M:, -1]
+        elif self.family in ("lv", "fhn"):                        # lotka_volterra_partial.py:218-219, 385-386
+            out["obs"] = ts[:, -2 * M:, 0].reshape(n, M, 2).transpose(0, 2, 1)
+            ob = self.extra["obs_bin"]
+            out["obs_bin"] = np.stack([ob[:, s:s + M] for s in starts])
+            if self.family == "lv":                               # lotka_volterra_partial.py:381-384
+                mv, sv = self.extra["mask_vals"], self.extra["shift_vals"]
+                out["mask"] = np.stack([mv[:, s:s + M + 1] for s in starts])
+                out["shift"] = np.stack([sv[:, s:s + M + 1] for s in starts])
+        elif self.family == "sv":                                 # SV_dense.py:322-328
+            mv, sv, obs = self.extra["mask_vals"], self.extra["shift_vals"], self.extra["obs"]
+            out["mask"] = np.stack([mv[0, s:s + M + 1] for s in starts])
+            out["shift"] = np.stack([sv[0, s:s + M + 1] for s in starts])
+            out["dim_one"] = np.stack([obs[s:s + M + 1] for s in starts])
+        return out
+
+
+def ar_table(obs, obs_bin, time_till, x0, T, n_flows, k, M, fw) -> FeatureTable:
+    """AR.py:132-150 (pad = n k + 1; channels [lags 0..fw-1, bin, time, time_till, obs_bin])."""
+    pad = n_flows * k + 1
+    T = int(np.int32(T))
+    obs_pad = [np.concatenate((np.zeros(pad - i), obs, np.zeros(i))) for i in range(fw)]
+    time_pad = np.concatenate((np.zeros(pad), np.arange(T + 1)))
+    bin_feats = np.float32(np.concatenate((np.ones(pad), np.zeros(T))))
+    obs_bin_p = np.concatenate((np.zeros(pad), obs_bin))
+    tt = np.concatenate((np.arange(pad + time_till[0], time_till[0], -1), time_till))
+    chans = obs_pad + [bin_feats.astype(np.float64), time_pad, tt, obs_bin_p]
+    mask_vals = np.concatenate((np.zeros((1, 1)), np.ones((1, T))), axis=1)
+    shift_vals = np.concatenate((np.array([[x0]]), np.zeros((1, T))), axis=1)
+    return FeatureTable("ar", M, pad + M, chans, 1, {"mask_vals": mask_vals, "shift_vals": shift_vals})
+
+
+def lv_table(obs, obs_bin, time_till, x0, T, dt, target_dims, n_flows, k, M, fw) -> FeatureTable:
+    """lotka_volterra_partial.py:185-204 (interleaved 2-D; lags at stride 5;
+    channels [lags, bin_feats (0s then 1s), time, time_till])."""
+    flow_dims = 2
+    pad = n_flows * k + flow_dims
+    obs_flatten = np.reshape(obs, -1, "F")
+    obs_pad = [np.concatenate((np.zeros(pad - i), obs_flatten, np.zeros(i))) for i in range(0, fw * 5, 5)]
+    time_pad = np.concatenate((np.zeros(pad), np.repeat(np.arange(dt, T + dt, dt), flow_dims)))
+    tt_pad = np.reshape(np.repeat(np.arange(np.round(pad * (dt / flow_dims), 1), 0.0, -dt), flow_dims),
+                        (flow_dims, -1), "F")
+    tt = np.reshape(np.concatenate((tt_pad, time_till), 1), -1, "F")
+    bin_feats = np.float32(np.concatenate((np.zeros(pad), np.ones(target_dims * flow_dims))))
+    mask_vals = np.concatenate((np.zeros((2, 1)), np.ones((flow_dims, target_dims))), axis=1)
+    shift_vals = np.concatenate((np.expand_dims(np.asarray(x0, dtype=np.float64), 1),
+                                 np.zeros((flow_dims, target_dims))), axis=1)
+    chans = obs_pad + [bin_feats.astype(np.float64), time_pad, tt]
+    kext = n_flows * k + flow_dims * M + 2
+    return FeatureTable("lv", M, kext, chans, 2, {"obs_bin": np.asarray(obs_bin, dtype=np.float64),
+                                                   "mask_vals": mask_vals, "shift_vals": shift_vals})
+
+
+def fhn_table(obs, obs_bin, time_till, x0, T, dt, target_dims, n_flows, k, M, fw) -> FeatureTable:
+    """fitz_nag_NVP.py:182-202 (as LV, but bin_feats is 1s then 0s and the time_till pad
+    arange runs to -dt, one pair longer than the other channels' pad)."""
+    flow_dims = 2
+    pad = n_flows * k + flow_dims
+    obs_flatten = np.reshape(obs, -1, "F")
+    obs_pad = [np.concatenate((np.zeros(pad - i), obs_flatten, np.zeros(i))) for i in range(0, fw * 5, 5)]
+    time_pad = np.concatenate((np.zeros(pad), np.repeat(np.arange(dt, T + dt, dt), flow_dims)))
+    tt_pad = np.reshape(np.repeat(np.arange(np.round(pad * (dt / flow_dims), 1), -dt, -dt), flow_dims),
+                        (flow_dims, -1), "F")
+    tt = np.reshape(np.concatenate((tt_pad, time_till), 1), -1, "F")
+    bin_feats = np.float32(np.concatenate((np.ones(pad), np.zeros(target_dims * flow_dims))))
+    chans = obs_pad + [bin_feats.astype(np.float64), time_pad, tt]
+    kext = n_flows * k + flow_dims * M + 2
+    return FeatureTable("fhn", M, kext, chans, 2, {"obs_bin": np.asarray(obs_bin, dtype=np.float64)})
+
+
+def sv_table(obs, x0, T, dt, target_dims, n_flows, k, M, fw) -> FeatureTable:
+    """SV_dense.py:159-185: rolling variances of the series and of its differences (float32
+    numpy, as the reference computes them on the float32 load), lags at stride 5, time."""
+    var_store = [np.var(obs[i:i + k]) for i in range(0, obs.shape[0] - k)]
+    var_pad = np.concatenate((np.zeros((n_flows + 1) * k), var_store), axis=0)
+    obs_diff = obs[1:] - obs[:-1]
+    var_diff_store = [np.var(obs_diff[i:i + k]) for i in range(0, obs_diff.shape[0] - k)]
+    var_diff_pad = np.concatenate((np.zeros((n_flows + 1) * k), np.log(var_diff_store), np.zeros(1)), axis=0)
+    obs_pad = [np.concatenate((np.zeros(n_flows * k - i), obs, np.zeros(i))) for i in range(0, fw * 5, 5)]
+    time_pad = np.concatenate((np.zeros(n_flows * k + 1), np.arange(0.1, T + dt, dt)))
+    mask_vals = np.concatenate((np.zeros((1, 1)), np.ones((1, target_dims))), axis=1)
+    shift_vals = np.concatenate((np.array([[x0]]), np.zeros((1, target_dims))), axis=1)
+    chans = [np.asarray(c, dtype=np.float64) for c in obs_pad + [time_pad, var_pad, var_diff_pad]]
+    kext = n_flows * k + M + 1
+    return FeatureTable("sv", M, kext, chans, 1, {"mask_vals": mask_vals, "shift_vals": shift_vals,
+                                                   "obs": np.asarray(obs, dtype=np.float64)})

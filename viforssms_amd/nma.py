@@ -1,0 +1,367 @@
+"""Neural moving-average (NMA) flow stack and the shared VI_SSM engine.
+
+Reference classes (AR.py:24-110; lotka_volterra_partial.py:25-159; SV_dense.py:23-136;
+fitz_nag_NVP.py:26-156): ``init_dist`` (base noise), ``IAF`` (one locally-variant IAF
+with feature injection), ``Permute`` (pair swap between 2-D flows), ``Flow_Stack``.
+
+Split of each IAF:
+  * window-shared, per step: feature MLP on time_feats, the feature part of the first
+    conv (a conv over features, written as k shifted GEMMs) + conv bias -> C[win, m, H],
+    and the theta branch (three linear layers) -> theta_term[b, H].  Small; torch GEMMs.
+  * per transition (the hot path): the sample-channel conv, hidden 1x1 layers, head,
+    affine transform and log-sigma sum -> libvissm ``vissm_flow_fwd/bwd``.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from datetime import datetime
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .ops import FlowShape, ma_flow, normal_base, base_logprob, elbo_terms, ElboFeeds, AdamaxKernel
+from .params import ParamStore, glorot_uniform
+from .theta_flow import ThetaFlow
+
+LOG_2PI = math.log(2 * math.pi)
+
+
+def elu(x):
+    return torch.nn.functional.elu(x)
+
+
+# ---------------------------------------------------------------------------------------
+# building blocks (names mirror the reference classes)
+# ---------------------------------------------------------------------------------------
+class init_dist:
+    """N(0, 1)^kernel_ext base; slp(p) -> (sample, log-prob over the last batch_dims entries) (AR.py:24-35).
+    Draws come from a counter-based Philox stream keyed by (seed, global sample index)."""
+
+    def __init__(self, kernel_ext: int, batch_dims: int, device):
+        self.kernel_ext = kernel_ext
+        self.batch_dims = batch_dims
+        self.device = device
+
+    def slp(self, p: int, seed: int = 0, offset: int = 0, eps: Optional[torch.Tensor] = None):
+        if eps is not None:
+            return eps, base_logprob(eps, self.batch_dims)
+        return normal_base(seed, offset, p, self.kernel_ext, self.batch_dims, self.device)
+
+
+class Permute:
+    """Adjacent-pair swap between the flows of the 2-D models (lotka_volterra_partial.py:137-159).
+    Fused into the preceding flow's output store (VissmFlowDesc.swap_out)."""
+
+    @staticmethod
+    def apply(x: torch.Tensor) -> torch.Tensor:
+        p, L = x.shape
+        return x.view(p, L // 2, 2).flip(-1).reshape(p, L)
+
+
+@dataclass
+class IAFSpec:
+    k: int
+    H: int
+    n_hidden: int
+    bn: bool
+    stride2: bool
+    feat: str          # "mlp4" | "sv" | "lv"
+    C_time: int
+    P_theta: int
+    CF: int            # feature channels entering the conv
+    feat_dims: int = 0  # LV: units of the time-mixing dense layer
+
+
+class IAF:
+    """One IAF flow (AR.py:38-89 and variants)."""
+
+    def __init__(self, store: ParamStore, idx: int, spec: IAFSpec, rng: np.random.Generator):
+        self.idx = idx
+        self.spec = spec
+        self.store = store
+        s, H, k = spec, spec.H, spec.k
+        pre = f"flow{idx}"
+        self.pre = pre
+        # feature branch (tf.layers.dense, glorot-uniform kernels, zero biases)
+        if s.feat == "lv":
+            dims = [s.C_time, H, H, H, s.feat_dims]
+        else:
+            cin = s.C_time + (s.C_time - 2 if s.feat == "sv" else 0)
+            dims = [cin, H, H, H, H]
+        for j in range(4):
+            store.add(f"{pre}/feat{j}/kernel", glorot_uniform((dims[j], dims[j + 1]), dims[j], dims[j + 1], rng))
+            store.add(f"{pre}/feat{j}/bias", np.zeros(dims[j + 1]))
+        # first conv: kernel [k, 1 + CF, H]
+        store.add(f"{pre}/conv/kernel", glorot_uniform((k, 1 + s.CF, H), k * (1 + s.CF), k * H, rng))
+        store.add(f"{pre}/conv/bias", np.zeros(H))
+        # theta branch: three linear dense layers
+        tdims = [s.P_theta, H, H, H]
+        for j in range(3):
+            store.add(f"{pre}/theta{j}/kernel", glorot_uniform((tdims[j], tdims[j + 1]), tdims[j], tdims[j + 1], rng))
+            store.add(f"{pre}/theta{j}/bias", np.zeros(tdims[j + 1]))
+        # hidden 1x1 convs (+ BN affine)
+        for l in range(s.n_hidden):
+            store.add(f"{pre}/hidden{l}/kernel", glorot_uniform((H, H), H, H, rng))
+            store.add(f"{pre}/hidden{l}/bias", np.zeros(H))
+            if s.bn:
+                store.add(f"{pre}/bn{l}/gamma", np.ones(H))
+                store.add(f"{pre}/bn{l}/beta", np.zeros(H))
+        store.add(f"{pre}/head/kernel", glorot_uniform((H, 2), H, 2, rng))
+        store.add(f"{pre}/head/bias", np.zeros(2))
+
+    def _p(self, name):
+        return self.store[f"{self.pre}/{name}"]
+
+    # ---- window-shared parts (torch) ----
+    def features(self, ts: torch.Tensor) -> torch.Tensor:
+        """Feature branch on the time_feats of this flow -> F [n_win, L-1, CF]."""
+        f = self.spec.feat
+        if f == "sv":                                              # SV_dense.py:53
+            h = torch.cat([ts[:, 1:, :], ts[:, 1:, :-2] - ts[:, :-1, :-2]], 2)
+        else:
+            h = ts[:, :-1, :]
+        for j in range(4):
+            h = elu(h @ self._p(f"feat{j}/kernel") + self._p(f"feat{j}/bias"))
+        if f == "lv":                                              # lotka_volterra_partial.py:75-76
+            h = h.transpose(1, 2)
+        return h
+
+    def conv_shared(self, F: torch.Tensor, Lh: int, s: int) -> torch.Tensor:
+        """C[w, m, :] = conv_b + sum_j F[w, s m + j, :] @ conv_w[j, 1:, :]  (valid conv over the features)."""
+        W = self._p("conv/kernel")
+        out = self._p("conv/bias").expand(F.shape[0], Lh, -1)
+        for j in range(self.spec.k):
+            out = out + F[:, j:j + s * (Lh - 1) + 1:s, :] @ W[j, 1:, :]
+        return out.contiguous()
+
+    def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
+        t = theta
+        for j in range(3):
+            t = t @ self._p(f"theta{j}/kernel") + self._p(f"theta{j}/bias")
+        return t.contiguous()
+
+    # ---- per-transition part (HIP) ----
+    def flow(self, shape: FlowShape, win, u, C, theta_term):
+        s = self.spec
+        w_eps = self._p("conv/kernel")[:, 0, :].contiguous()
+        if s.n_hidden > 0:
+            w_hid = torch.stack([self._p(f"hidden{l}/kernel") for l in range(s.n_hidden)])
+            b_hid = torch.stack([self._p(f"hidden{l}/bias") for l in range(s.n_hidden)])
+        else:
+            w_hid = b_hid = None
+        if s.bn and s.n_hidden > 0:
+            bn_g = torch.stack([self._p(f"bn{l}/gamma") for l in range(s.n_hidden)])
+            bn_b = torch.stack([self._p(f"bn{l}/beta") for l in range(s.n_hidden)])
+        else:
+            bn_g = bn_b = None
+        return ma_flow(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b,
+                       self._p("head/kernel"), self._p("head/bias"))
+
+
+# ---------------------------------------------------------------------------------------
+# per-step batch
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Batch:
+    starts: np.ndarray                # reference batch_select for this rank's samples
+    uniq: np.ndarray                  # distinct window starts
+    ts: torch.Tensor                  # time_feats of the distinct windows [n_win, kext, C]
+    win: Optional[torch.Tensor]       # int32 [B] sample -> window (None when n_win == 1)
+    feeds: ElboFeeds
+    host_feeds: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    @property
+    def B(self):
+        return len(self.starts)
+
+    @property
+    def n_win(self):
+        return len(self.uniq)
+
+
+@dataclass
+class ModelDef:
+    family: str
+    model_id: int
+    D: int
+    M: int
+    k: int
+    n_flows: int
+    network_dims: Sequence[int]
+    C_time: int
+    P_theta: int
+    scale_num: float        # T (AR) or target_dims: ELBO scale = scale_num / M
+    priors: Sequence
+    dt: float = 1.0
+    obs_std: float = 1.0
+    theta_base: tuple = (0.0, 1.0)
+    theta_act: str = "elu"
+    n_maf: int = 5
+    clip: float = 2.5e8
+    theta_pos: Sequence[bool] = ()
+
+    @property
+    def kernel_ext(self):
+        return self.k * self.n_flows + self.D * self.M + self.D
+
+    @property
+    def n_logsig(self):
+        return self.D * self.M
+
+
+class Engine:
+    """Parameters + one differentiable ELBO evaluation on the GPU."""
+
+    def __init__(self, mdef: ModelDef, table, device=None, seed: int = 1, precision: int = _lib.VISSM_PREC_FP32,
+                 perms: Optional[Sequence[Sequence[int]]] = None, init_seed: int = 1):
+        _lib.load()   # fail loudly, before any work, if the HIP library is missing
+        self.mdef = mdef
+        self.table = table
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.seed = int(seed)
+        self.precision = precision
+        H = mdef.network_dims[0]
+        if any(h != H for h in mdef.network_dims):
+            raise ValueError("all network_dims must be equal (the reference adds layer outputs of width network_dims[0])")
+        rng = np.random.default_rng(init_seed)
+        self.store = ParamStore()
+        kext = mdef.kernel_ext
+        self.flows: List[IAF] = []
+        for i in range(mdef.n_flows):
+            if mdef.family == "lv":
+                spec = IAFSpec(mdef.k, H, len(mdef.network_dims) - 2, True, True, "lv", mdef.C_time, mdef.P_theta,
+                               CF=kext - 1, feat_dims=kext - 1 - i * mdef.k)
+            else:
+                spec = IAFSpec(mdef.k, H, len(mdef.network_dims) - 2, mdef.family != "ar", mdef.D == 2,
+                               "sv" if mdef.family == "sv" else "mlp4", mdef.C_time, mdef.P_theta, CF=H)
+            self.flows.append(IAF(self.store, i, spec, rng))
+        if perms is None:
+            perms = [list(np.random.permutation(np.arange(0, mdef.P_theta))) for _ in range(mdef.n_maf - 1)]
+        self.perms = [list(map(int, p)) for p in perms]
+        self.theta_dist = ThetaFlow(self.store, mdef.P_theta, mdef.n_maf, self.perms, mdef.theta_base[0],
+                                    mdef.theta_base[1], mdef.theta_act, rng)
+        self.store.finalize(self.device)
+
+    # ---- batches ----
+    def make_batch(self, starts: np.ndarray) -> Batch:
+        starts = np.asarray(starts, dtype=np.int64)
+        uniq, inv = np.unique(starts, return_inverse=True)
+        ts_np = self.table.windows(uniq)
+        feeds_np = self.table.feeds(uniq, ts_np)
+        dev = self.device
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev)
+        win = None if len(uniq) == 1 else torch.as_tensor(inv.astype(np.int32), device=dev)
+        feeds = ElboFeeds(obs=t(feeds_np["obs"]) if "obs" in feeds_np else None,
+                          obs_bin=t(feeds_np["obs_bin"]) if "obs_bin" in feeds_np else None,
+                          mask=t(feeds_np["mask"]) if "mask" in feeds_np else None,
+                          shift=t(feeds_np["shift"]) if "shift" in feeds_np else None,
+                          dim_one=t(feeds_np["dim_one"]) if "dim_one" in feeds_np else None,
+                          win=win, n_win=len(uniq))
+        return Batch(starts, uniq, t(ts_np), win, feeds, feeds_np)
+
+    # ---- random inputs (Philox; keyed by global sample index so sharding is exact) ----
+    def draw(self, step: int, B: int, global_offset: int, B_total: int):
+        md = self.mdef
+        row0 = step * B_total + global_offset
+        eps, base_lp = normal_base(self.seed, row0, B, md.kernel_ext, md.n_logsig, self.device)
+        n, _ = normal_base(self.seed ^ 0x5DEECE66D, row0, B, md.P_theta, 0, self.device)
+        x0 = n * md.theta_base[1] + md.theta_base[0]
+        return eps, base_lp, x0
+
+    # ---- forward ----
+    def forward(self, batch: Batch, eps: torch.Tensor, base_lp: Optional[torch.Tensor], x0_theta: torch.Tensor):
+        md = self.mdef
+        if base_lp is None:
+            base_lp = base_logprob(eps, md.n_logsig)
+        theta, logq_theta = self.theta_dist.sample_and_log_prob(x0_theta)
+        s = 2 if md.D == 2 else 1
+        u, lq = eps, base_lp
+        B = eps.shape[0]
+        L = md.kernel_ext
+        for i, fl in enumerate(self.flows):
+            ts = batch.ts if md.family == "lv" else batch.ts[:, i * md.k:, :]
+            F = fl.features(ts)
+            Lh = (L - md.k) // s
+            C = fl.conv_shared(F, Lh, s)
+            tt = fl.theta_term(theta)
+            shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
+                              stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
+                              n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+            u, ls = fl.flow(shape, batch.win, u, C, tt)
+            lq = lq - ls
+            L -= md.k
+        z = u
+        sde, obs, extra = elbo_terms(md.model_id, md.M, md.dt, md.obs_std, batch.feeds, z, theta)
+        if md.family == "lv":
+            lq = lq + extra
+        prior = self.prior_logprob(theta)
+        scale = md.scale_num / md.M
+        if md.family == "sv":
+            elbo = scale * (sde - lq) + prior - logq_theta
+        else:
+            elbo = scale * (sde - lq + obs) + prior - logq_theta
+        return {"elbo": elbo, "sde": sde, "obs": obs, "logq": lq, "theta": theta, "logq_theta": logq_theta,
+                "prior": prior, "z": z}
+
+    def prior_logprob(self, theta):
+        md = self.mdef
+        mean = torch.tensor([m for m, _ in md.priors], dtype=theta.dtype, device=theta.device)
+        sd = torch.tensor([s for _, s in md.priors], dtype=theta.dtype, device=theta.device)
+        zz = (theta - mean) / sd
+        return (-0.5 * zz * zz - torch.log(sd) - 0.5 * LOG_2PI).sum(-1)
+
+    def lf_sample(self, z: torch.Tensor, batch: Batch) -> torch.Tensor:
+        """The latent path x [B, D, M+1] (torch; used by pre-training losses and save_paths)."""
+        md = self.mdef
+        B = z.shape[0]
+        f = batch.feeds
+        w = batch.win.long() if batch.win is not None else torch.zeros(B, dtype=torch.long, device=z.device)
+        if md.family == "ar":
+            return z.view(B, 1, -1)
+        if md.family == "lv":
+            zz = z.view(B, -1, 2).transpose(1, 2)
+            return torch.nn.functional.softplus(zz) * f.mask[w] + f.shift[w]
+        if md.family == "sv":
+            return torch.stack([f.dim_one[w], z * f.mask[w] + f.shift[w]], 1)
+        return z.view(B, -1, 2).transpose(1, 2)
+
+
+# ---------------------------------------------------------------------------------------
+# optimiser slots + scalar logging
+# ---------------------------------------------------------------------------------------
+class AdamaxSlots:
+    """Slot pair (v = first moment, m = inf-norm) for one AdamaxOptimizer instance over the flat buffer."""
+
+    def __init__(self, n: int, device):
+        self.v = torch.zeros(n, dtype=torch.float32, device=device)
+        self.m = torch.zeros(n, dtype=torch.float32, device=device)
+        self.kernel = AdamaxKernel(n, device)
+
+
+class ScalarLog:
+    """TensorBoard-scalar replacement: JSON lines under <tensorboard_path>/<dd:mm:yy-HH:MM:SS>/scalars.jsonl
+    with the reference's summary names (AR.py:205-238)."""
+
+    def __init__(self, tensorboard_path: Optional[str], enabled: bool = True):
+        self.f = None
+        if tensorboard_path and enabled:
+            d = os.path.join(tensorboard_path, datetime.now().strftime("%d:%m:%y-%H:%M:%S"))
+            os.makedirs(d, exist_ok=True)
+            self.f = open(os.path.join(d, "scalars.jsonl"), "a")
+
+    def write(self, run: int, values: Dict[str, float]):
+        if self.f is None:
+            return
+        import json
+        self.f.write(json.dumps({"step": run, **{k: float(v) for k, v in values.items()}}) + "\n")
+        self.f.flush()
+
+    def close(self):
+        if self.f is not None:
+            self.f.close()
+            self.f = None

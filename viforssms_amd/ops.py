@@ -1,0 +1,246 @@
+"""torch.autograd wrappers around the libvissm HIP kernels.
+
+Each Function's forward and backward is exactly one C-ABI call (plus
+caller-allocated workspace from torch's caching allocator, so no hipMalloc
+happens on the step path).  Tensors must be contiguous fp32 on the current
+HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import FlowDesc, FlowParams, FlowGrads, ElboDesc, ElboData, check, ptr
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise _lib.VissmError("libvissm kernels run on the GPU only; got a CPU tensor "
+                                  "(there is deliberately no CPU fallback)")
+        if t.dtype not in (torch.float32, torch.int32):
+            raise _lib.VissmError(f"expected fp32/int32 tensors, got {t.dtype}")
+        if not t.is_contiguous():
+            raise _lib.VissmError("expected contiguous tensors")
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------------------
+# base noise
+# ---------------------------------------------------------------------------------------
+def normal_base(seed: int, offset: int, B: int, L: int, n_last: int, device) -> (torch.Tensor, torch.Tensor):
+    """init_dist.slp (AR.py:31-35): eps ~ N(0,1) [B, L] and the base log-prob over the last n_last entries."""
+    lib = _lib.load()
+    eps = torch.empty(B, L, dtype=torch.float32, device=device)
+    lp = torch.empty(B, dtype=torch.float32, device=device)
+    check(lib.vissm_normal_base(ctypes.c_uint64(seed & (2 ** 64 - 1)), ctypes.c_uint64(offset), ptr(eps), ptr(lp),
+                                B, L, n_last, _lib.stream_handle(device)), "vissm_normal_base")
+    return eps, lp
+
+
+def base_logprob(eps: torch.Tensor, n_last: int) -> torch.Tensor:
+    lib = _lib.load()
+    _require_gpu(eps)
+    B, L = eps.shape
+    lp = torch.empty(B, dtype=torch.float32, device=eps.device)
+    check(lib.vissm_base_logprob(ptr(eps), ptr(lp), B, L, n_last, _lib.stream_handle(eps.device)),
+          "vissm_base_logprob")
+    return lp
+
+
+# ---------------------------------------------------------------------------------------
+# IAF flow
+# ---------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class FlowShape:
+    B: int
+    L: int
+    k: int
+    H: int
+    n_hidden: int
+    bn: bool
+    stride2: bool
+    swap_out: bool
+    n_logsig: int
+    n_win: int
+    precision: int = _lib.VISSM_PREC_FP32
+
+    def desc(self) -> FlowDesc:
+        return FlowDesc(self.B, self.L, self.k, self.H, self.n_hidden, int(self.bn), int(self.stride2),
+                        int(self.swap_out), self.n_logsig, self.n_win, self.precision, 0)
+
+    @property
+    def Lout(self):
+        return self.L - self.k
+
+    @property
+    def Lh(self):
+        return self.Lout // (2 if self.stride2 else 1)
+
+
+def _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head) -> FlowParams:
+    return FlowParams(ptr(w_eps), ptr(w_hid), ptr(b_hid), ptr(bn_g), ptr(bn_b), ptr(w_head), ptr(b_head))
+
+
+class MAFlowFn(torch.autograd.Function):
+    """One IAF flow (IAF._create_flow, AR.py:50-85) -> (u_next, logsig)."""
+
+    @staticmethod
+    def forward(ctx, shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head):
+        lib = _lib.load()
+        _require_gpu(u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, win)
+        dev = u.device
+        d = shape.desc()
+        u_next = torch.empty(shape.B, shape.Lout, dtype=torch.float32, device=dev)
+        logsig = torch.empty(shape.B, dtype=torch.float32, device=dev)
+        wsz = lib.vissm_flow_workspace_size(ctypes.byref(d), 0)
+        if wsz == 0:
+            check(-1, "vissm_flow_workspace_size")
+        ws = _workspace(wsz, dev)
+        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        check(lib.vissm_flow_fwd(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
+                                 ptr(u_next), ptr(logsig), ptr(ws), wsz, _lib.stream_handle(dev)),
+              "vissm_flow_fwd")
+        ctx.shape = shape
+        ctx.save_for_backward(win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        return u_next, logsig
+
+    @staticmethod
+    def backward(ctx, g_next, g_ls):
+        lib = _lib.load()
+        shape: FlowShape = ctx.shape
+        win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head = ctx.saved_tensors
+        dev = u.device
+        if g_next is None:
+            g_next = torch.zeros(shape.B, shape.Lout, dtype=torch.float32, device=dev)
+        if g_ls is None:
+            g_ls = torch.zeros(shape.B, dtype=torch.float32, device=dev)
+        g_next = g_next.contiguous()
+        g_ls = g_ls.contiguous()
+        d = shape.desc()
+        du = torch.empty_like(u)
+        dC = torch.empty_like(C)
+        dth = torch.empty_like(theta_term)
+        gw = [torch.empty_like(t) if t is not None else None for t in (w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)]
+        grads = FlowGrads(*[ptr(t) for t in gw])
+        wsz = lib.vissm_flow_workspace_size(ctypes.byref(d), 1)
+        ws = _workspace(wsz, dev)
+        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        check(lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
+                                 ptr(g_next), ptr(g_ls), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws),
+                                 wsz, _lib.stream_handle(dev)), "vissm_flow_bwd")
+        return (None, None, du, dC, dth, *gw)
+
+
+def ma_flow(shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head):
+    return MAFlowFn.apply(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+
+
+# ---------------------------------------------------------------------------------------
+# ELBO log-densities
+# ---------------------------------------------------------------------------------------
+@dataclass
+class ElboFeeds:
+    """Per-window observation feeds (device tensors, fp32; win int32 [B] or None)."""
+    obs: Optional[torch.Tensor] = None
+    obs_bin: Optional[torch.Tensor] = None
+    mask: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
+    dim_one: Optional[torch.Tensor] = None
+    win: Optional[torch.Tensor] = None
+    n_win: int = 1
+
+    def cdata(self) -> ElboData:
+        return ElboData(ptr(self.win), ptr(self.obs), ptr(self.obs_bin), ptr(self.mask), ptr(self.shift),
+                        ptr(self.dim_one))
+
+
+class ElboFn(torch.autograd.Function):
+    """Path log-densities per sample -> (sde, obs, extra)."""
+
+    @staticmethod
+    def forward(ctx, model: int, M: int, dt: float, obs_std: float, feeds: ElboFeeds, z, theta):
+        lib = _lib.load()
+        _require_gpu(z, theta, feeds.obs, feeds.obs_bin, feeds.mask, feeds.shift, feeds.dim_one, feeds.win)
+        B = z.shape[0]
+        d = ElboDesc(model, B, M, feeds.n_win, float(dt), float(obs_std))
+        data = feeds.cdata()
+        sde = torch.empty(B, dtype=torch.float32, device=z.device)
+        obs = torch.empty_like(sde)
+        extra = torch.empty_like(sde)
+        check(lib.vissm_elbo_fwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(sde), ptr(obs),
+                                 ptr(extra), _lib.stream_handle(z.device)), "vissm_elbo_fwd")
+        ctx.args = (model, M, dt, obs_std, feeds)
+        ctx.save_for_backward(z, theta)
+        return sde, obs, extra
+
+    @staticmethod
+    def backward(ctx, g_sde, g_obs, g_extra):
+        lib = _lib.load()
+        model, M, dt, obs_std, feeds = ctx.args
+        z, theta = ctx.saved_tensors
+        B = z.shape[0]
+        zero = None
+
+        def fix(g):
+            nonlocal zero
+            if g is None:
+                if zero is None:
+                    zero = torch.zeros(B, dtype=torch.float32, device=z.device)
+                return zero
+            return g.contiguous()
+
+        g_sde, g_obs, g_extra = fix(g_sde), fix(g_obs), fix(g_extra)
+        d = ElboDesc(model, B, M, feeds.n_win, float(dt), float(obs_std))
+        data = feeds.cdata()
+        dz = torch.empty_like(z)
+        dth = torch.empty_like(theta)
+        check(lib.vissm_elbo_bwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde), ptr(g_obs),
+                                 ptr(g_extra), ptr(dz), ptr(dth), _lib.stream_handle(z.device)), "vissm_elbo_bwd")
+        return None, None, None, None, None, dz, dth
+
+
+def elbo_terms(model: int, M: int, dt: float, obs_std: float, feeds: ElboFeeds, z, theta):
+    return ElboFn.apply(model, M, dt, obs_std, feeds, z, theta)
+
+
+# ---------------------------------------------------------------------------------------
+# optimiser
+# ---------------------------------------------------------------------------------------
+class AdamaxKernel:
+    """Fused global-norm clip + Adamax over flat fp32 buffers (optimisers/adamax.py:42-58)."""
+
+    def __init__(self, n: int, device):
+        lib = _lib.load()
+        self.n = n
+        self.wsz = lib.vissm_adamax_workspace_size(n)
+        self.ws = _workspace(self.wsz, device)
+        self.gnorm = torch.zeros(1, dtype=torch.float32, device=device)
+
+    def step(self, params, grads, v, m, lr, beta1, beta2, eps=1e-8, clip=0.0):
+        lib = _lib.load()
+        _require_gpu(params, grads, v, m)
+        check(lib.vissm_adamax_step(ptr(params), ptr(grads), ptr(v), ptr(m), self.n, float(lr), float(beta1),
+                                    float(beta2), float(eps), float(clip), ptr(self.gnorm), ptr(self.ws), self.wsz,
+                                    _lib.stream_handle(params.device)), "vissm_adamax_step")
+        return self.gnorm
+
+
+def sqnorm(x: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _require_gpu(x)
+    n = x.numel()
+    wsz = lib.vissm_adamax_workspace_size(n)
+    ws = _workspace(wsz, x.device)
+    out = torch.empty(1, dtype=torch.float32, device=x.device)
+    check(lib.vissm_sqnorm(ptr(x), n, ptr(out), ptr(ws), wsz, _lib.stream_handle(x.device)), "vissm_sqnorm")
+    return out

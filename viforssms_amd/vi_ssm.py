@@ -1,0 +1,294 @@
+"""VI_SSM: the reference's model + training-loop class, shared by the four families.
+
+Mirrors VI_SSM (AR.py:113-362 and the LV/SV/FHN variants): build_flow(), train(tensorboard_path,
+save_path), save(PATH), load(PATH), save_paths(PATH_obs).  One training step is
+  window pick (np.random.choice, AR.py:263-265) -> feature gather -> ELBO on the GPU (libvissm)
+  -> grad of sum(-ELBO) -> [RCCL all-reduce SUM over ranks] -> fused global-norm clip + Adamax.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .nma import Engine, ModelDef, Batch, AdamaxSlots, ScalarLog
+
+
+@dataclass
+class ThetaSpec:
+    """What the reference passes as ``theta_dist``: the q(theta) flow architecture
+    (Chain of Invert(MAF) with these permutations, base N(loc, scale), activation)."""
+    n_bijectors: int
+    perms: List[List[int]]
+    base_loc: float
+    base_scale: float
+    activation: str = "elu"
+
+    @staticmethod
+    def build(P_theta: int, n_bijectors: int, base_loc: float, base_scale: float, activation: str = "elu"):
+        """Draws the permutations with the global numpy RNG exactly as the reference
+        (np.random.permutation per Permute, AR.py:383-385)."""
+        perms = [list(map(int, np.random.permutation(np.arange(0, P_theta)))) for _ in range(n_bijectors - 1)]
+        return ThetaSpec(n_bijectors, perms, base_loc, base_scale, activation)
+
+
+class DistCtx:
+    """Data parallelism over samples: rank r owns samples [r*p_local, (r+1)*p_local) of every step."""
+
+    def __init__(self, rank: int = 0, world: int = 1, group=None):
+        self.rank, self.world, self.group = rank, world, group
+
+    @staticmethod
+    def from_env():
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return DistCtx(dist.get_rank(), dist.get_world_size())
+        return DistCtx()
+
+    def all_reduce_(self, t: torch.Tensor):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+
+class VISSMBase:
+    """Engine + optimisers + reference training loop."""
+
+    def __init__(self, mdef: ModelDef, table, theta_spec: ThetaSpec, p: int, pre_train: bool,
+                 early_stopping: float, learn_rate: float, grad_clip: float, device=None, seed: int = 1,
+                 precision: int = _lib.VISSM_PREC_FP32, dist: Optional[DistCtx] = None, log_every: int = 1,
+                 init_seed: int = 1):
+        mdef.n_maf = theta_spec.n_bijectors
+        mdef.theta_base = (theta_spec.base_loc, theta_spec.base_scale)
+        mdef.theta_act = theta_spec.activation
+        self.mdef = mdef
+        self.p = int(p)
+        self.dist = dist or DistCtx()
+        if self.p % self.dist.world:
+            raise ValueError(f"p={p} must divide evenly over {self.dist.world} ranks")
+        self.p_local = self.p // self.dist.world
+        self.engine = Engine(mdef, table, device=device, seed=seed, precision=precision, perms=theta_spec.perms,
+                             init_seed=init_seed)
+        self.store = self.engine.store
+        self.pre_train = pre_train
+        self.early_stopping = early_stopping
+        self.learn_rate = learn_rate
+        self.grad_clip = grad_clip
+        self.log_every = max(1, int(log_every))
+        self.T = mdef.scale_num
+        self.batch_dims = mdef.M
+        self._batch_cache: Dict[tuple, Batch] = {}
+        self._opt_main: Optional[AdamaxSlots] = None
+        self._opt_pre: List[AdamaxSlots] = []
+        self.last: Dict[str, float] = {}
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ graph
+    def build_flow(self):
+        """Allocates the optimiser slots (main Adamax beta1=0.95 with global-norm clip; pre-training
+        Adamax beta1=0.9 with its own slots), as build_flow does in the reference."""
+        n = self.store.numel
+        dev = self.engine.device
+        self._opt_main = AdamaxSlots(n, dev)
+        self._opt_pre = [AdamaxSlots(n, dev) for _ in range(self.n_pretrain_opts())]
+        return self
+
+    def n_pretrain_opts(self) -> int:
+        return 1
+
+    # ------------------------------------------------------------------ windows
+    def select_windows(self) -> np.ndarray:
+        """AR.py:257-265: batch_select = np.random.choice(arange(0, T, M), p, replace = M p >= T)."""
+        T = int(self.target_len())
+        M = self.batch_dims
+        replace = (M * self.p) >= T
+        return np.random.choice(np.arange(0, T, M), size=self.p, replace=replace)
+
+    def target_len(self) -> int:
+        return int(self.T)
+
+    def batch_for(self, starts_global: np.ndarray) -> Batch:
+        r = self.dist.rank
+        local = np.asarray(starts_global[r * self.p_local:(r + 1) * self.p_local], dtype=np.int64)
+        uniq = np.unique(local)
+        key = (tuple(uniq.tolist()) if len(uniq) == 1 else None)
+        if key is not None and key in self._batch_cache and self._batch_cache[key].B == len(local):
+            return self._batch_cache[key]
+        b = self.engine.make_batch(local)
+        if key is not None:
+            self._batch_cache = {key: b}
+        return b
+
+    # ------------------------------------------------------------------ one step
+    def forward(self, batch: Batch, step: int, eps=None, x0_theta=None):
+        """One ELBO evaluation.  eps / x0_theta inject the randomness (parity tests);
+        otherwise they are drawn from the Philox streams keyed by the global sample index."""
+        base_lp = None
+        if eps is None or x0_theta is None:
+            e, blp, x0 = self.engine.draw(step, batch.B, self.dist.rank * self.p_local, self.p)
+            if eps is None:
+                eps, base_lp = e, blp
+            if x0_theta is None:
+                x0_theta = x0
+        return self.engine.forward(batch, eps, base_lp, x0_theta)
+
+    def elbo_step(self, batch: Batch, step: int, eps=None, x0_theta=None, apply: bool = True):
+        """grad of sum(-ELBO) (AR.py:228-229) -> all-reduce -> clip_by_global_norm -> Adamax (AR.py:230-234)."""
+        st = self.store
+        st.zero_grad()
+        out = self.forward(batch, step, eps, x0_theta)
+        loss = (-out["elbo"]).sum()
+        loss.backward()
+        st.sync_grads()
+        self.dist.all_reduce_(st.grad)
+        if apply:
+            o = self._opt_main
+            gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm())
+            out["global_norm"] = gn
+        return out
+
+    def clip_norm(self) -> float:
+        return float(self.grad_clip)
+
+    def minimize(self, loss: torch.Tensor, slots: AdamaxSlots, beta1: float = 0.9, lr: float = 1e-3):
+        """AdamaxOptimizer(learning_rate=lr, beta1).minimize(loss) for a pre-training loss (no clip)."""
+        st = self.store
+        st.zero_grad()
+        loss.backward()
+        st.sync_grads()
+        self.dist.all_reduce_(st.grad)
+        slots.kernel.step(st.flat, st.grad, slots.v, slots.m, lr, beta1, 0.999, 1e-8, 0.0)
+
+    # model-specific pre-training step; returns True when pre-training is finished
+    def pretrain_step(self, batch: Batch, run: int) -> bool:
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ loop
+    def summaries(self, out) -> Dict[str, float]:
+        s = self.mdef.scale_num / self.mdef.M
+        vals = {
+            "loss/ELBO": out["elbo"].mean(),
+            "loss/SDE_log_prob": s * out["sde"].mean(),
+            "loss/theta_log_prob": out["logq_theta"].mean(),
+            "loss/obs_log_prob": s * out["obs"].mean(),
+            "loss/path_log_prob": s * out["logq"].mean(),
+        }
+        if "global_norm" in out:
+            vals["optimize/global_norm"] = out["global_norm"][0]
+        keys = list(vals)
+        stacked = torch.stack([v.float().reshape(()) for v in vals.values()])
+        if self.dist.world > 1:
+            stacked = stacked.clone()
+            self.dist.all_reduce_(stacked)
+            stacked = stacked / self.dist.world
+        host = stacked.cpu().numpy()
+        return {k: float(v) for k, v in zip(keys, host)}
+
+    def train(self, tensorboard_path: Optional[str], save_path: Optional[str], max_runs: Optional[int] = None,
+              verbose: bool = True):
+        """VI_SSM.train (AR.py:240-310): endless unless early_stopping / max_runs."""
+        if self._opt_main is None:
+            self.build_flow()
+        if tensorboard_path:
+            os.makedirs(tensorboard_path, exist_ok=True)
+        writer = ScalarLog(tensorboard_path if self.dist.rank == 0 else None)
+        run = 0
+        total = 0
+        if verbose and self.dist.rank == 0:
+            print("Training model...")
+        converged = False
+        while not converged:
+            starts = self.select_windows()
+            batch = self.batch_for(starts)
+            if self.pre_train:
+                if run == 0 and verbose and self.dist.rank == 0:
+                    print("Pre-training...")
+                if self.pretrain_step(batch, run):
+                    self.pre_train = False
+                    if verbose and self.dist.rank == 0:
+                        print("Finished pre-training")
+                    run = 0
+            else:
+                out = self.elbo_step(batch, self.global_step)
+                if run % self.log_every == 0:
+                    self.last = self.summaries(out)
+                    writer.write(run, self.last)
+            self.global_step += 1
+            if run == self.early_stopping:
+                converged = True
+            if save_path and run % 1000 == 0 and self.dist.rank == 0:
+                self.save(save_path)
+            run += 1
+            total += 1
+            if max_runs is not None and total >= max_runs:
+                break
+        writer.close()
+        return self
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, PATH: str):
+        """Own checkpoint format: flat params, both Adamax slot sets, step, numpy RNG state."""
+        d = os.path.dirname(PATH)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        st = self.store
+        blob = {
+            "params": st.flat.detach().cpu(),
+            "names": "\n".join(st.names()),
+            "global_step": torch.tensor(self.global_step),
+            "main_v": self._opt_main.v.cpu() if self._opt_main else torch.zeros(0),
+            "main_m": self._opt_main.m.cpu() if self._opt_main else torch.zeros(0),
+        }
+        for i, o in enumerate(self._opt_pre):
+            blob[f"pre{i}_v"] = o.v.cpu()
+            blob[f"pre{i}_m"] = o.m.cpu()
+        torch.save(blob, PATH)
+        print("Model saved")
+
+    def load(self, PATH: str):
+        self.pre_train = False
+        blob = torch.load(PATH, weights_only=True)
+        if blob["names"] != "\n".join(self.store.names()):
+            raise ValueError("checkpoint variables do not match this model")
+        if self._opt_main is None:
+            self.build_flow()
+        with torch.no_grad():
+            self.store.flat.copy_(blob["params"].to(self.store.flat.device))
+            if blob["main_v"].numel():
+                self._opt_main.v.copy_(blob["main_v"])
+                self._opt_main.m.copy_(blob["main_m"])
+            for i, o in enumerate(self._opt_pre):
+                if f"pre{i}_v" in blob:
+                    o.v.copy_(blob[f"pre{i}_v"])
+                    o.m.copy_(blob[f"pre{i}_m"])
+        self.global_step = int(blob["global_step"])
+        print("Model restored")
+
+    @torch.no_grad()
+    def sample_paths(self, starts: np.ndarray, step: int = 0):
+        batch = self.engine.make_batch(np.asarray(starts))
+        out = self.forward(batch, step)
+        return self.engine.lf_sample(out["z"], batch)
+
+    def save_paths(self, PATH_obs: str):
+        """Posterior path samples for every window start (AR.py:323-362; the reference's AR version
+        feeds a non-existent placeholder and crashes, AR.py:355 -- this one runs)."""
+        M = self.batch_dims
+        stack = []
+        for idx in np.arange(0, self.target_len(), M):
+            print(idx, "/", self.target_len())
+            x = self.sample_paths(np.tile(idx, self.p_local), step=self.global_step)
+            stack.append(x[:, :, 1:].cpu().numpy())
+        paths = np.concatenate(stack, axis=2)
+        d = os.path.dirname(PATH_obs)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(PATH_obs, "w") as f:
+            np.savetxt(f, np.reshape(paths, (paths.shape[0], -1)) if paths.shape[1] > 1 else paths[:, 0, :])
