@@ -38,7 +38,7 @@ def build_model(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_lay
     if family == "ar":
         from viforssms_amd.ar import VI_SSM
         T = T or M
-        obs, ob, tt = _ar_data(T, seed, impute=2)
+        obs, ob, tt = _ar_data(T, seed, impute=2 if T % 2 == 0 else 1)
         priors = [(0.0, 10.0)] * 3
         spec = ThetaSpec(5, [list(rng.permutation(3)) for _ in range(4)], 1.5, 0.5, "elu")
         model = VI_SSM(obs, 1.0, 10.0, spec, priors, T, B, k, M, nd, n_flows, fw, ob, tt, device=device,
