@@ -1,0 +1,90 @@
+// C-ABI entry points of the IAF flow (include/vissm.h): argument validation and
+// dispatch to the implementation.  flow2 (matrix cores, exact fp32) is the
+// product path; flow1 (LDS-tiled VALU fp32) is kept as an independent second
+// implementation for A/B checks, selected with VISSM_FLOW_IMPL=1.
+#include "common.hpp"
+
+#include <cstdlib>
+
+namespace vissm {
+
+size_t flow1_workspace_size(const VissmFlowDesc* d, int backward);
+int flow1_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              float*, float*, void*, size_t, hipStream_t);
+int flow1_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
+size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
+int flow2_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              float*, float*, void*, size_t, hipStream_t);
+int flow2_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
+
+static int impl() {
+  static int v = [] {
+    const char* e = std::getenv("VISSM_FLOW_IMPL");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
+
+static int validate(const VissmFlowDesc* d) {
+  VISSM_CHECK_ARG(d, "flow: null desc");
+  VISSM_CHECK_ARG(d->B >= 1 && d->k >= 1 && d->k <= 64 && d->H >= 1 && d->H <= 64, "flow: bad B/k/H (B=%d k=%d H=%d)",
+                  d->B, d->k, d->H);
+  VISSM_CHECK_ARG(d->n_hidden >= 0 && d->n_hidden <= 4, "flow: n_hidden=%d not in [0,4]", d->n_hidden);
+  VISSM_CHECK_ARG(d->L > d->k, "flow: L=%d must exceed k=%d", d->L, d->k);
+  VISSM_CHECK_ARG(!d->stride2 || ((d->L - d->k) % 2 == 0), "flow: stride-2 output length must be even");
+  VISSM_CHECK_ARG(!d->swap_out || ((d->L - d->k) % 2 == 0), "flow: swap_out needs an even output length");
+  VISSM_CHECK_ARG(d->n_logsig >= 0 && d->n_logsig <= d->L - d->k, "flow: bad n_logsig");
+  VISSM_CHECK_ARG(d->n_win >= 1, "flow: n_win must be >= 1");
+  VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32, "flow: precision %d not supported by this build", d->precision);
+  return VISSM_OK;
+}
+
+}  // namespace vissm
+
+using namespace vissm;
+
+extern "C" {
+
+size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
+  if (validate(d) != VISSM_OK) return 0;
+  return impl() == 1 ? flow1_workspace_size(d, backward) : flow2_workspace_size(d, backward);
+}
+
+int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+                   const int32_t* win, const float* theta_term, float* u_next, float* logsig, void* workspace,
+                   size_t ws_bytes, void* stream) {
+  int rc = validate(d);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && u && C && theta_term && u_next && logsig, "flow_fwd: null pointer");
+  VISSM_CHECK_ARG(w->w_eps && w->w_head && w->b_head && (d->n_hidden == 0 || (w->w_hid && w->b_hid)),
+                  "flow_fwd: null weight pointer");
+  VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (w->bn_g && w->bn_b), "flow_fwd: bn needs bn_g/bn_b");
+  VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
+  hipStream_t st = as_stream(stream);
+  return impl() == 1 ? flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st)
+                     : flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+}
+
+int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+                   const int32_t* win, const float* theta_term, const float* du_next, const float* dlogsig,
+                   float* du, float* dC, float* dtheta_term, const VissmFlowGrads* gr, void* workspace,
+                   size_t ws_bytes, void* stream) {
+  int rc = validate(d);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && du && dC && dtheta_term && gr,
+                  "flow_bwd: null pointer");
+  VISSM_CHECK_ARG(gr->w_eps && gr->w_head && gr->b_head && (d->n_hidden == 0 || (gr->w_hid && gr->b_hid)),
+                  "flow_bwd: null grad pointer");
+  VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (gr->bn_g && gr->bn_b && w->bn_g && w->bn_b),
+                  "flow_bwd: bn needs bn_g/bn_b pointers");
+  VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
+  hipStream_t st = as_stream(stream);
+  return impl() == 1 ? flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                                 ws_bytes, st)
+                     : flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                                 ws_bytes, st);
+}
+
+}  // extern "C"

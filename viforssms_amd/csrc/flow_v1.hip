@@ -630,26 +630,9 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   return a;
 }
 
-static int validate(const VissmFlowDesc* d) {
-  VISSM_CHECK_ARG(d, "flow: null desc");
-  VISSM_CHECK_ARG(d->B >= 1 && d->k >= 1 && d->k <= 64 && d->H >= 1 && d->H <= 64, "flow: bad B/k/H (B=%d k=%d H=%d)",
-                  d->B, d->k, d->H);
-  VISSM_CHECK_ARG(d->n_hidden >= 0 && d->n_hidden <= 4, "flow: n_hidden=%d not in [0,4]", d->n_hidden);
-  VISSM_CHECK_ARG(d->L > d->k, "flow: L=%d must exceed k=%d", d->L, d->k);
-  VISSM_CHECK_ARG(!d->stride2 || ((d->L - d->k) % 2 == 0), "flow: stride-2 output length must be even");
-  VISSM_CHECK_ARG(!d->swap_out || ((d->L - d->k) % 2 == 0), "flow: swap_out needs an even output length");
-  VISSM_CHECK_ARG(d->n_logsig >= 0 && d->n_logsig <= d->L - d->k, "flow: bad n_logsig");
-  VISSM_CHECK_ARG(d->n_win >= 1, "flow: n_win must be >= 1");
-  VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32, "flow: precision %d not supported by the fp32 path",
-                  d->precision);
-  return VISSM_OK;
-}
-
 }  // namespace flow1
-}  // namespace vissm
 
-using namespace vissm;
-using namespace vissm::flow1;
+using namespace flow1;
 
 #define FLOW_DISPATCH(NHV, KERNEL, ...)                                                 \
   switch (NHV) {                                                                        \
@@ -660,26 +643,19 @@ using namespace vissm::flow1;
     default: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                         \
   }
 
-extern "C" {
 
-size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
-  if (validate(d) != VISSM_OK) return 0;
+size_t flow1_workspace_size(const VissmFlowDesc* d, int backward) {
   Geom g = geom(d, backward != 0);
   return backward ? bwd_ws_layout(d, g, nullptr, nullptr) : fwd_ws_layout(d, g, nullptr, nullptr);
 }
 
-int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
-                   const int32_t* win, const float* theta_term, float* u_next, float* logsig, void* workspace,
-                   size_t ws_bytes, void* stream) {
-  int rc = validate(d);
-  if (rc) return rc;
-  VISSM_CHECK_ARG(w && u && C && theta_term && u_next && logsig, "flow_fwd: null pointer");
-  VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
+int flow1_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+              const int32_t* win, const float* theta_term, float* u_next, float* logsig, void* workspace,
+              size_t ws_bytes, hipStream_t st) {
   Geom g = geom(d, false);
   VISSM_CHECK_ARG(workspace && ws_bytes >= fwd_ws_layout(d, g, nullptr, nullptr), "flow_fwd: workspace too small");
   WsF ws;
   fwd_ws_layout(d, g, reinterpret_cast<char*>(workspace), &ws);
-  hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(prep_weights_kernel, dim3(1), dim3(256), 0, st, *w, d->H, d->k, d->n_hidden, d->bn, ws.wp,
                      nullptr, ws.bh, ws.bng, ws.bnb, ws.weps, nullptr, ws.whead);
   VISSM_CHECK_LAUNCH("flow_prep");
@@ -694,24 +670,15 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   return launch_reduce_rows(ws.ls_slab, logsig, g.n_chunks, d->B, st);
 }
 
-int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
-                   const int32_t* win, const float* theta_term, const float* du_next, const float* dlogsig,
-                   float* du, float* dC, float* dtheta_term, const VissmFlowGrads* gr, void* workspace,
-                   size_t ws_bytes, void* stream) {
-  int rc = validate(d);
-  if (rc) return rc;
-  VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && du && dC && dtheta_term && gr,
-                  "flow_bwd: null pointer");
-  VISSM_CHECK_ARG(gr->w_eps && gr->w_head && gr->b_head && (d->n_hidden == 0 || (gr->w_hid && gr->b_hid)),
-                  "flow_bwd: null grad pointer");
-  VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (gr->bn_g && gr->bn_b && w->bn_g && w->bn_b),
-                  "flow_bwd: bn needs bn_g/bn_b pointers");
-  VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
+int flow1_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+              const int32_t* win, const float* theta_term, const float* du_next, const float* dlogsig,
+              float* du, float* dC, float* dtheta_term, const VissmFlowGrads* gr, void* workspace,
+              size_t ws_bytes, hipStream_t st) {
+  int rc;
   Geom g = geom(d, true);
   VISSM_CHECK_ARG(workspace && ws_bytes >= bwd_ws_layout(d, g, nullptr, nullptr), "flow_bwd: workspace too small");
   WsB ws;
   bwd_ws_layout(d, g, reinterpret_cast<char*>(workspace), &ws);
-  hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(prep_weights_kernel, dim3(1), dim3(256), 0, st, *w, d->H, d->k, d->n_hidden, d->bn, ws.wp,
                      ws.wTp, ws.bh, ws.bng, ws.bnb, ws.weps, ws.wepsT, ws.whead);
   VISSM_CHECK_LAUNCH("flow_prep");
@@ -750,4 +717,5 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   return VISSM_OK;
 }
 
-}  // extern "C"
+
+}  // namespace vissm
