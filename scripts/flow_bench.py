@@ -1,0 +1,81 @@
+"""Flow-kernel micro-benchmark: times vissm_flow_fwd / vissm_flow_bwd alone at a given shape,
+interleaving implementations in one process (A/B), and cross-checks their outputs."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from viforssms_amd import _lib  # noqa: E402
+from viforssms_amd.ops import FlowShape, MAFlowFn  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=16384)
+    ap.add_argument("--T", type=int, default=5000)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--H", type=int, default=50)
+    ap.add_argument("--nh", type=int, default=1)
+    ap.add_argument("--stride2", action="store_true")
+    ap.add_argument("--impls", default="2,3")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--only", default="", help="run only this impl (for PMC passes)")
+    args = ap.parse_args()
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    D = 2 if args.stride2 else 1
+    L = 3 * args.k + D * args.T + D
+    B, k, H, nh = args.B, args.k, args.H, args.nh
+    sh = FlowShape(B=B, L=L, k=k, H=H, n_hidden=nh, bn=nh > 1, stride2=args.stride2, swap_out=False,
+                   n_logsig=D * args.T, n_win=1)
+    r = lambda *s, sc=1.0: (torch.randn(*s, generator=g, device=dev) * sc).contiguous()
+    u = r(B, L)
+    C = r(1, sh.Lh, H, sc=0.3)
+    tt = r(B, H, sc=0.3)
+    w_eps, w_hid, b_hid = r(k, H, sc=0.3), r(nh, H, H, sc=0.15), r(nh, H, sc=0.1)
+    bn_g, bn_b = (1 + r(nh, H, sc=0.1), r(nh, H, sc=0.1)) if nh > 1 else (None, None)
+    w_head, b_head = r(H, 2, sc=0.2), r(2, sc=0.1)
+    gnext, gls = r(B, sh.Lout), r(B)
+    impls = [int(x) for x in (args.only or args.impls).split(",")]
+    res = {}
+    outs = {}
+    for rd in range(args.rounds):
+        for im in impls:
+            lib.vissm_flow_set_impl(im)
+            ins = [t.clone().requires_grad_(True) for t in (u, C, tt, w_eps, w_hid, b_hid, w_head, b_head)]
+            extra = [bn_g, bn_b]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            un, ls = MAFlowFn.apply(sh, None, ins[0], ins[1], ins[2], ins[3], ins[4], ins[5], extra[0], extra[1],
+                                    ins[6], ins[7])
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            torch.autograd.backward([un, ls], [gnext, gls])
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            res.setdefault(im, []).append((t1 - t0, t2 - t1))
+            if rd == 0:
+                outs[im] = [un.detach(), ls.detach()] + [t.grad for t in ins]
+    summary = {}
+    for im, v in res.items():
+        f = sorted(x[0] for x in v[1:] or v)
+        b = sorted(x[1] for x in v[1:] or v)
+        summary[im] = {"fwd_ms": 1e3 * f[len(f) // 2], "bwd_ms": 1e3 * b[len(b) // 2]}
+    if len(outs) > 1:
+        ks = sorted(outs)
+        a0 = outs[ks[0]]
+        for im in ks[1:]:
+            errs = [float((x - y).norm() / (y.norm() + 1e-30)) for x, y in zip(outs[im], a0)]
+            summary[im]["max_rel_diff_vs_%d" % ks[0]] = max(errs)
+    print(json.dumps({"shape": vars(args), "results": summary}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,8 @@
 // C-ABI entry points of the IAF flow (include/vissm.h): argument validation and
-// dispatch to the implementation.  flow2 (matrix cores, exact fp32) is the
-// product path; flow1 (LDS-tiled VALU fp32) is kept as an independent second
-// implementation for A/B checks, selected with VISSM_FLOW_IMPL=1.
+// dispatch to the implementation.  flow3 (matrix cores, exact fp32, 8-wave
+// blocks) is the product path; flow2 (4-wave blocks) and flow1 (LDS-tiled VALU
+// fp32) are kept as independent implementations for A/B checks, selected with
+// VISSM_FLOW_IMPL=2 / VISSM_FLOW_IMPL=1.
 #include "common.hpp"
 
 #include <cstdlib>
@@ -14,17 +15,24 @@ int flow1_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 int flow1_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
+size_t flow3_workspace_size(const VissmFlowDesc* d, int backward);
+int flow3_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              float*, float*, void*, size_t, hipStream_t);
+int flow3_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 int flow2_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               float*, float*, void*, size_t, hipStream_t);
 int flow2_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 
+static int g_impl = 0;  // 0 = not chosen yet
+
 static int impl() {
-  static int v = [] {
+  if (g_impl == 0) {
     const char* e = std::getenv("VISSM_FLOW_IMPL");
-    return (e && e[0] == '1') ? 1 : 2;
-  }();
-  return v;
+    g_impl = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
+  }
+  return g_impl;
 }
 
 static int validate(const VissmFlowDesc* d) {
@@ -47,9 +55,20 @@ using namespace vissm;
 
 extern "C" {
 
+int vissm_flow_set_impl(int32_t which) {
+  VISSM_CHECK_ARG(which >= 0 && which <= 3, "flow_set_impl: %d not in [0,3]", which);
+  const int prev = impl();
+  if (which > 0) vissm::g_impl = which;
+  return prev;
+}
+
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
-  return impl() == 1 ? flow1_workspace_size(d, backward) : flow2_workspace_size(d, backward);
+  switch (impl()) {
+    case 1: return flow1_workspace_size(d, backward);
+    case 2: return flow2_workspace_size(d, backward);
+    default: return flow3_workspace_size(d, backward);
+  }
 }
 
 int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
@@ -63,8 +82,11 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (w->bn_g && w->bn_b), "flow_fwd: bn needs bn_g/bn_b");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
-  return impl() == 1 ? flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st)
-                     : flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+  switch (impl()) {
+    case 1: return flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+    case 2: return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+    default: return flow3_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+  }
 }
 
 int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
@@ -81,10 +103,14 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                   "flow_bwd: bn needs bn_g/bn_b pointers");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
-  return impl() == 1 ? flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                                 ws_bytes, st)
-                     : flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                                 ws_bytes, st);
+  switch (impl()) {
+    case 1: return flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                             ws_bytes, st);
+    case 2: return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                             ws_bytes, st);
+    default: return flow3_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                              ws_bytes, st);
+  }
 }
 
 }  // extern "C"

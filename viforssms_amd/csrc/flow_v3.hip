@@ -24,13 +24,13 @@
 #include "common.hpp"
 
 namespace vissm {
-namespace flow2 {
+namespace flow3 {
 
 constexpr int P = 32;    // head positions per tile (MFMA columns: 2 blocks of 16)
 constexpr int S = 16;    // samples per group
 constexpr int HP = 64;   // padded hidden width
 constexpr int PS = 33;   // LDS row stride of [h][p] tiles
-constexpr int NT = 256;
+constexpr int NT = 512;  // 8 waves: wave w owns row block w & 3 and column block w >> 2
 constexpr int US = 2 * P + 64 + 8;  // u window staging
 
 using f4 = __attribute__((ext_vector_type(4))) float;
@@ -167,130 +167,113 @@ struct Smem {
   float dz[HP][PS];           // gradient scratch [h][p]
   float us[US];               // u window
   float go[2 * P];            // upstream gradient of the tile's outputs
-  float red[4][2][P];         // head partial sums per wave
+  float red[4][2][P];         // head partial sums per row block
   float mu[P], rr[P], sig[P], gmu[P], gr[P];
   float ths[HP];              // theta term of the sample
   float bng[NH > 0 ? NH : 1][HP], bnb[NH > 0 ? NH : 1][HP];
 };
 
+struct Lane {
+  int lane, w, rb, cb, li, lk;
+  __device__ Lane() {
+    lane = threadIdx.x & 63;
+    w = threadIdx.x >> 6;
+    rb = w & 3;
+    cb = w >> 2;
+    li = lane & 15;
+    lk = lane >> 4;
+  }
+  __device__ int row(int r) const { return 16 * rb + 4 * lk + r; }  // accumulator row r of this lane
+  __device__ int col() const { return 16 * cb + li; }              // accumulator column of this lane
+};
+
 // ---------------------------------------------------------------------------
-// forward of one work unit.  On return: act[] filled, xh[cb][r] (the head's
-// input for this lane's rows/cols) in registers, mu/rr/sig in LDS.
+// forward of one work unit.  On return: act[] filled, xh (the head's input at
+// this lane's rows/column) in registers, mu/rr/sig in LDS.
 // ---------------------------------------------------------------------------
 template <int NH, int HK, int KS>
-__device__ __forceinline__ void unit_forward(const KArgs& a, Smem<NH>& sm, const WImg& W, const f4 (&cinit)[2],
-                                             f4 (&xh)[2]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int li = lane & 15, lk = lane >> 4;
+__device__ __forceinline__ void unit_forward(const KArgs& a, Smem<NH>& sm, const WImg& W, const f4& cinit, f4& xh) {
+  const Lane L;
+  const int p = L.col();
   // ---- layer 0: A0^T = W_eps^T U + C^T + theta ----
-  f4 acc[2];
+  f4 acc = cinit;
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    acc[cb] = cinit[cb];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[cb][r] += sm.ths[16 * w + 4 * lk + r];
-  }
+  for (int r = 0; r < 4; ++r) acc[r] += sm.ths[L.row(r)];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const int j = 4 * s + lk;
-    const float wa = W.weps[j * HP + 16 * w + li];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) acc[cb] = mma(wa, sm.us[a.s * (16 * cb + li) + j], acc[cb]);
+    const int j = 4 * s + L.lk;
+    acc = mma(W.weps[j * HP + 16 * L.rb + L.li], sm.us[a.s * p + j], acc);
   }
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = 16 * w + 4 * lk + r;
-      const float e = h < a.H ? elu_f(acc[cb][r]) : 0.f;
-      acc[cb][r] = e;
-      sm.act[0][h][16 * cb + li] = e;
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int h = L.row(r);
+    const float e = h < a.H ? elu_f(acc[r]) : 0.f;
+    acc[r] = e;
+    sm.act[0][h][p] = e;
+  }
   // ---- hidden layers ----
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     __syncthreads();
-    f4 z[2];
+    f4 z;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) z[cb][r] = W.bh[l * HP + 16 * w + 4 * lk + r];
+    for (int r = 0; r < 4; ++r) z[r] = W.bh[l * HP + L.row(r)];
     const float* wl = W.wp + l * HP * HP;
 #pragma unroll 4
     for (int s = 0; s < HK; ++s) {
-      const int hin = 4 * s + lk;
-      const float wa = wl[hin * HP + 16 * w + li];
-      float g = 1.f, be = 0.f;
-      if (l > 0) {
-        g = sm.bng[l - 1][hin];
-        be = sm.bnb[l - 1][hin];
-      }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) z[cb] = mma(wa, fmaf(g, sm.act[l][hin][16 * cb + li], be), z[cb]);
+      const int hin = 4 * s + L.lk;
+      float x = sm.act[l][hin][p];
+      if (l > 0) x = fmaf(sm.bng[l - 1][hin], x, sm.bnb[l - 1][hin]);
+      z = mma(wl[hin * HP + 16 * L.rb + L.li], x, z);
     }
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int h = 16 * w + 4 * lk + r;
-        const float e = h < a.H ? elu_f(z[cb][r]) : 0.f;
-        sm.act[l + 1][h][16 * cb + li] = e;
-        acc[cb][r] = a.bn ? fmaf(sm.bng[l][h], e, sm.bnb[l][h]) : e;
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int h = L.row(r);
+      const float e = h < a.H ? elu_f(z[r]) : 0.f;
+      sm.act[l + 1][h][p] = e;
+      acc[r] = a.bn ? fmaf(sm.bng[l][h], e, sm.bnb[l][h]) : e;
+    }
   }
   // ---- head: mu, r = X_nh . w_head + b ----
   {
-    float pm[2], pr[2];
+    float m = 0.f, q = 0.f;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      float m = 0.f, q = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int h = 16 * w + 4 * lk + r;
-        m = fmaf(acc[cb][r], W.whead[h], m);
-        q = fmaf(acc[cb][r], W.whead[HP + h], q);
-      }
-      m += __shfl_xor(m, 16, 64);
-      m += __shfl_xor(m, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      pm[cb] = m;
-      pr[cb] = q;
-      xh[cb] = acc[cb];
+    for (int r = 0; r < 4; ++r) {
+      const int h = L.row(r);
+      m = fmaf(acc[r], W.whead[h], m);
+      q = fmaf(acc[r], W.whead[HP + h], q);
     }
-    if (lk == 0) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        sm.red[w][0][16 * cb + li] = pm[cb];
-        sm.red[w][1][16 * cb + li] = pr[cb];
-      }
+    m += __shfl_xor(m, 16, 64);
+    m += __shfl_xor(m, 32, 64);
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    xh = acc;
+    if (L.lk == 0) {
+      sm.red[L.rb][0][p] = m;
+      sm.red[L.rb][1][p] = q;
     }
   }
   __syncthreads();
   if (threadIdx.x < P) {
-    const int p = threadIdx.x;
-    const float m = sm.red[0][0][p] + sm.red[1][0][p] + sm.red[2][0][p] + sm.red[3][0][p] + W.whead[2 * HP];
-    const float q = sm.red[0][1][p] + sm.red[1][1][p] + sm.red[2][1][p] + sm.red[3][1][p] + W.whead[2 * HP + 1];
-    sm.mu[p] = m;
-    sm.rr[p] = q;
-    sm.sig[p] = softplus_f(q) + 1e-10f;
+    const int pp = threadIdx.x;
+    const float m = sm.red[0][0][pp] + sm.red[1][0][pp] + sm.red[2][0][pp] + sm.red[3][0][pp] + W.whead[2 * HP];
+    const float q = sm.red[0][1][pp] + sm.red[1][1][pp] + sm.red[2][1][pp] + sm.red[3][1][pp] + W.whead[2 * HP + 1];
+    sm.mu[pp] = m;
+    sm.rr[pp] = q;
+    sm.sig[pp] = softplus_f(q) + 1e-10f;
   }
   __syncthreads();
 }
 
-// initial accumulator = C^T tile for the lane's rows / columns
+// initial accumulator = C^T tile at the lane's rows / column
 __device__ __forceinline__ void load_cinit(const KArgs& a, const float* __restrict__ C, int win, int m0, int nP,
-                                           f4 (&ci)[2]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int li = lane & 15, lk = lane >> 4;
+                                           f4& ci) {
+  const Lane L;
+  const int p = L.col();
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int p = 16 * cb + li;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = 16 * w + 4 * lk + r;
-      ci[cb][r] = (p < nP && h < a.H) ? C[(static_cast<size_t>(win) * a.Lh + m0 + p) * a.H + h] : 0.f;
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int h = L.row(r);
+    ci[r] = (p < nP && h < a.H) ? C[(static_cast<size_t>(win) * a.Lh + m0 + p) * a.H + h] : 0.f;
   }
 }
 
@@ -304,9 +287,8 @@ __device__ __forceinline__ void load_unit_inputs(const KArgs& a, Smem<NH>& sm, c
 }
 
 template <int NH>
-__device__ __forceinline__ void load_bn(const KArgs& a, Smem<NH>& sm, const WImg& W) {
-  const int tid = threadIdx.x;
-  for (int i = tid; i < (NH > 0 ? NH : 1) * HP; i += NT) {
+__device__ __forceinline__ void load_bn(Smem<NH>& sm, const WImg& W) {
+  for (int i = threadIdx.x; i < (NH > 0 ? NH : 1) * HP; i += NT) {
     (&sm.bng[0][0])[i] = NH > 0 ? W.bng[i] : 1.f;
     (&sm.bnb[0][0])[i] = NH > 0 ? W.bnb[i] : 0.f;
   }
@@ -316,7 +298,7 @@ __device__ __forceinline__ void load_bn(const KArgs& a, Smem<NH>& sm, const WImg
 // forward kernel: samples outer, tiles inner
 // ---------------------------------------------------------------------------
 template <int NH, int HK, int KS>
-__global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+__global__ __launch_bounds__(NT, 4) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     WImg W, float* __restrict__ u_next,
                                                     float* __restrict__ ls_slab) {
@@ -324,7 +306,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
   const int tid = threadIdx.x;
   const int g = blockIdx.x, c = blockIdx.y;
   const int m_lo = c * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
-  load_bn<NH>(a, sm, W);
+  load_bn<NH>(sm, W);
   for (int bl = 0; bl < a.S; ++bl) {
     const int b = g * a.S + bl;
     if (b >= a.B) break;
@@ -337,7 +319,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
       const int t0 = a.s * m0;
       __syncthreads();
       load_unit_inputs<NH>(a, sm, ub, tht + static_cast<size_t>(b) * a.H, t0);
-      f4 ci[2], xh[2];
+      f4 ci, xh;
       load_cinit(a, C, wi, m0, nP, ci);
       __syncthreads();
       unit_forward<NH, HK, KS>(a, sm, W, ci, xh);
@@ -379,44 +361,48 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
                                                     float* __restrict__ halo) {
   __shared__ Smem<NH> sm;
   __shared__ float carry[S][64];
-  __shared__ float dth[S][HP];
+  __shared__ float dth[2][S][HP];   // per column block, summed in fixed order at chunk end
   __shared__ float dul[US];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lk = lane >> 4;
+  const Lane L;
+  const int tid = threadIdx.x;
+  const int li = L.li, lk = L.lk, rb = L.rb, cb = L.cb;
+  const int pcol = L.col();
   const int g = blockIdx.x, c = blockIdx.y;
   const int m_lo = c * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = g * a.S, nb = min(a.S, a.B - b_lo);
   constexpr int NHA = NH > 0 ? NH : 1;
-  constexpr int njb = (4 * KS + 15) >> 4;  // row blocks of dW_eps / dcon (j)
+  constexpr int njb = (4 * KS + 15) >> 4;   // row blocks (j) of dW_eps / dcon
+  constexpr int njw = (njb + 1) / 2;        // dW_eps j blocks per wave (jb = cb + 2 i)
 
-  // weight-gradient accumulators (wave w: rows 16w..16w+15 of dW_l; column block w of dW_eps)
-  f4 dWl[NHA][4];
-  f4 dWe[njb];
+  // weight-gradient accumulators: dW_l rows h_in = 16 rb + 4 lk + r, columns h_out blocks 2 cb, 2 cb + 1;
+  // dW_eps rows j = 16 (cb + 2 i) + 4 lk + r, column h = 16 rb + li
+  f4 dWl[NHA][2];
+  f4 dWe[njw];
   float dbl[NHA][4], dgl[NHA][4], dbe[NHA][4];
   float dwh0[4], dwh1[4];
   float dbh0 = 0.f, dbh1 = 0.f;
 #pragma unroll
-  for (int l = 0; l < NHA; ++l)
+  for (int l = 0; l < NHA; ++l) {
+    dWl[l][0] = dWl[l][1] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dWl[l][r] = f4{0.f, 0.f, 0.f, 0.f};
-      dbl[l][r] = dgl[l][r] = dbe[l][r] = 0.f;
-    }
+    for (int r = 0; r < 4; ++r) dbl[l][r] = dgl[l][r] = dbe[l][r] = 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) dwh0[r] = dwh1[r] = 0.f;
 #pragma unroll
-  for (int r = 0; r < njb; ++r) dWe[r] = f4{0.f, 0.f, 0.f, 0.f};
-  load_bn<NH>(a, sm, W);
+  for (int i = 0; i < njw; ++i) dWe[i] = f4{0.f, 0.f, 0.f, 0.f};
+  load_bn<NH>(sm, W);
   for (int i = tid; i < S * 64; i += NT) {
     (&carry[0][0])[i] = 0.f;
-    (&dth[0][0])[i] = 0.f;
+    (&dth[0][0][0])[i] = 0.f;
+    (&dth[1][0][0])[i] = 0.f;
   }
 
   for (int m0 = m_lo; m0 < m_hi; m0 += P) {
     const int nP = min(P, m_hi - m0);
     const int t0 = a.s * m0;
-    f4 dCa[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-    f4 ci[2];
+    f4 dCa = f4{0.f, 0.f, 0.f, 0.f};
+    f4 ci;
     int cached = -1;
 
     for (int bl = 0; bl < nb; ++bl) {
@@ -430,13 +416,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const int o = t0 + q;
         sm.go[q] = (q < a.s * nP) ? gb[a.swap_out ? (o ^ 1) : o] : 0.f;
       }
-      for (int q = tid; q < US; q += NT) dul[q] = 0.f;
       if (wi != cached) {
         load_cinit(a, C, wi, m0, nP, ci);
         cached = wi;
       }
       __syncthreads();
-      f4 xh[2];
+      f4 xh;
       unit_forward<NH, HK, KS>(a, sm, W, ci, xh);
 
       // ---- head backward (per position) ----
@@ -454,16 +439,15 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         dbh1 += dr;
       }
       __syncthreads();
-      f4 dx[2];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const float gm = sm.gmu[16 * cb + li], gq = sm.gr[16 * cb + li];
+      f4 dx;
+      {
+        const float gm = sm.gmu[pcol], gq = sm.gr[pcol];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int h = 16 * w + 4 * lk + r;
-          dx[cb][r] = W.whead[h] * gm + W.whead[HP + h] * gq;
-          dwh0[r] = fmaf(xh[cb][r], gm, dwh0[r]);
-          dwh1[r] = fmaf(xh[cb][r], gq, dwh1[r]);
+          const int h = L.row(r);
+          dx[r] = W.whead[h] * gm + W.whead[HP + h] * gq;
+          dwh0[r] = fmaf(xh[r], gm, dwh0[r]);
+          dwh1[r] = fmaf(xh[r], gq, dwh1[r]);
         }
       }
 
@@ -471,35 +455,31 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
       for (int l = NH - 1; l >= 0; --l) {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int h = 16 * w + 4 * lk + r;
-            const float e = sm.act[l + 1][h][16 * cb + li];
-            float de = dx[cb][r];
-            if (a.bn) {
-              dgl[l][r] = fmaf(de, e, dgl[l][r]);
-              dbe[l][r] += de;
-              de *= sm.bng[l][h];
-            }
-            const float dzv = de * elu_grad_from_out(e);
-            dbl[l][r] += dzv;
-            sm.dz[h][16 * cb + li] = dzv;
+        for (int r = 0; r < 4; ++r) {
+          const int h = L.row(r);
+          const float e = sm.act[l + 1][h][pcol];
+          float de = dx[r];
+          if (a.bn) {
+            dgl[l][r] = fmaf(de, e, dgl[l][r]);
+            dbe[l][r] += de;
+            de *= sm.bng[l][h];
           }
+          const float dzv = de * elu_grad_from_out(e);
+          dbl[l][r] += dzv;
+          sm.dz[h][pcol] = dzv;
+        }
         __syncthreads();
-        // dX_l[h_in][p] = sum_h_out W[h_in][h_out] dz[h_out][p]   (rows h_in of this wave)
-        f4 nx[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+        // dX_l[h_in][p] = sum_h_out W[h_in][h_out] dz[h_out][p]
+        f4 nx = f4{0.f, 0.f, 0.f, 0.f};
         const float* wt = W.wtp + l * HP * HP;
 #pragma unroll 4
         for (int s = 0; s < HK; ++s) {
           const int ho = 4 * s + lk;
-          const float wa = wt[ho * HP + 16 * w + li];
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) nx[cb] = mma(wa, sm.dz[ho][16 * cb + li], nx[cb]);
+          nx = mma(wt[ho * HP + 16 * rb + li], sm.dz[ho][pcol], nx);
         }
-        // dW_l[h_in][h_out] += sum_p X_l[h_in][p] dz[h_out][p]   (h_in rows 16w.., all h_out blocks)
+        // dW_l[h_in][h_out] += sum_p X_l[h_in][p] dz[h_out][p]
         {
-          const int hin = 16 * w + li;
+          const int hin = 16 * rb + li;
           float gi = 1.f, bi = 0.f;
           if (l > 0) {
             gi = sm.bng[l - 1][hin];
@@ -510,70 +490,57 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
             const int p = 4 * s + lk;
             const float xa = fmaf(gi, sm.act[l][hin][p], bi);
 #pragma unroll
-            for (int ob = 0; ob < 4; ++ob) dWl[l][ob] = mma(xa, sm.dz[16 * ob + li][p], dWl[l][ob]);
+            for (int o = 0; o < 2; ++o) dWl[l][o] = mma(xa, sm.dz[16 * (2 * cb + o) + li][p], dWl[l][o]);
           }
         }
         __syncthreads();
-        dx[0] = nx[0];
-        dx[1] = nx[1];
+        dx = nx;
       }
 
       // ---- first layer ----
       {
-        float rs[4] = {0.f, 0.f, 0.f, 0.f};
+        float rs[4];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int h = 16 * w + 4 * lk + r;
-            const int p = 16 * cb + li;
-            const float da = (p < nP) ? dx[cb][r] * elu_grad_from_out(sm.act[0][h][p]) : 0.f;
-            dCa[cb][r] += da;
-            rs[r] += da;
-            sm.dz[h][p] = da;
-          }
+        for (int r = 0; r < 4; ++r) {
+          const int h = L.row(r);
+          const float da = (pcol < nP) ? dx[r] * elu_grad_from_out(sm.act[0][h][pcol]) : 0.f;
+          dCa[r] += da;
+          rs[r] = da;
+          sm.dz[h][pcol] = da;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = sum16(rs[r]);
-          if (li == 0) dth[bl][16 * w + 4 * lk + r] += v;
+          if (li == 0) dth[cb][bl][L.row(r)] += v;
         }
       }
       __syncthreads();
-      // dW_eps[j][h] += sum_p U[j][p] dA0[h][p]   (wave w: h block w, all j blocks)
+      // dW_eps[j][h] += sum_p U[j][p] dA0[h][p]   (h block rb; j blocks cb, cb + 2, ...)
 #pragma unroll
       for (int s = 0; s < P / 4; ++s) {
         const int p = 4 * s + lk;
-        const float bz = sm.dz[16 * w + li][p];
+        const float bz = sm.dz[16 * rb + li][p];
 #pragma unroll
-        for (int jb = 0; jb < njb; ++jb) dWe[jb] = mma(sm.us[a.s * p + 16 * jb + li], bz, dWe[jb]);
+        for (int i = 0; i < njw; ++i) {
+          const int jb = cb + 2 * i;
+          if (jb < njb) dWe[i] = mma(sm.us[a.s * p + 16 * jb + li], bz, dWe[i]);
+        }
       }
-      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]  (block pairs (jb, cb) spread over waves)
-      f4 dcn[2];
-      int npair = 0;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int pair = w + 4 * q;
-        dcn[q] = f4{0.f, 0.f, 0.f, 0.f};
-        if (pair < 2 * njb) {
-          const int jb = pair >> 1, cb = pair & 1;
+      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]   (wave w: block pair w = (jb, column block))
+      f4 dcn = f4{0.f, 0.f, 0.f, 0.f};
+      const bool has_pair = L.w < 2 * njb;
+      const int pjb = L.w >> 1, pcb = L.w & 1;
+      if (has_pair) {
 #pragma unroll 4
-          for (int s = 0; s < HK; ++s) {
-            const int hh = 4 * s + lk;
-            dcn[q] = mma(W.wepsT[hh * HP + 16 * jb + li], sm.dz[hh][16 * cb + li], dcn[q]);
-          }
-          npair = q + 1;
+        for (int s = 0; s < HK; ++s) {
+          const int hh = 4 * s + lk;
+          dcn = mma(W.wepsT[hh * HP + 16 * pjb + li], sm.dz[hh][16 * pcb + li], dcn);
         }
       }
       __syncthreads();
-      // park dcon in act[0] (free now): [j][p]
+      if (has_pair) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (q < npair) {
-          const int pair = w + 4 * q;
-          const int jb = pair >> 1, cb = pair & 1;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sm.act[0][16 * jb + 4 * lk + r][16 * cb + li] = dcn[q][r];
-        }
+        for (int r = 0; r < 4; ++r) sm.act[0][16 * pjb + 4 * lk + r][16 * pcb + li] = dcn[r];  // park dcon [j][p]
       }
       __syncthreads();
       // du over local positions q in [0, s*nP + k)
@@ -606,12 +573,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 
     // dC tile of this group
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int h = 16 * w + 4 * lk + r, p = 16 * cb + li;
-        if (p < nP && h < a.H) dC_slab[(static_cast<size_t>(g) * a.Lh + m0 + p) * a.H + h] = dCa[cb][r];
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int h = L.row(r);
+      if (pcol < nP && h < a.H) dC_slab[(static_cast<size_t>(g) * a.Lh + m0 + pcol) * a.H + h] = dCa[r];
+    }
   }  // tiles
 
   __syncthreads();
@@ -621,47 +586,48 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       if (c == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = carry[bl][q];
       else halo[(static_cast<size_t>(b) * a.n_chunks + c) * a.k + q] = carry[bl][q];
     }
-    if (tid < a.H) dth_slab[(static_cast<size_t>(c) * a.B + b) * a.H + tid] = dth[bl][tid];
+    if (tid < a.H) dth_slab[(static_cast<size_t>(c) * a.B + b) * a.H + tid] = dth[0][bl][tid] + dth[1][bl][tid];
   }
 
   // ---- weight-gradient partials of this block ----
   const int H = a.H;
   const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
   float* ws = dW_slab + (static_cast<size_t>(g) * a.n_chunks + c) * nW;
-  // w_eps [k][H]: dWe[jb][r] = dW_eps[j = 16 jb + 4 lk + r][h = 16 w + li]
 #pragma unroll
-  for (int jb = 0; jb < njb; ++jb)
+  for (int i = 0; i < njw; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int j = 16 * jb + 4 * lk + r, h = 16 * w + li;
-      if (j < a.k && h < H) ws[j * H + h] = dWe[jb][r];
+      const int j = 16 * (cb + 2 * i) + 4 * lk + r, h = 16 * rb + li;
+      if (cb + 2 * i < njb && j < a.k && h < H) ws[j * H + h] = dWe[i][r];
     }
   int off = a.k * H;
-  // w_hid [l][h_in][h_out]: dWl[l][ob][r] = dW[h_in = 16 w + 4 lk + r][h_out = 16 ob + li]
 #pragma unroll
   for (int l = 0; l < NH; ++l)
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
+    for (int o = 0; o < 2; ++o)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int hi = 16 * w + 4 * lk + r, ho = 16 * ob + li;
-        if (hi < H && ho < H) ws[off + (l * H + hi) * H + ho] = dWl[l][ob][r];
+        const int hi = L.row(r), ho = 16 * (2 * cb + o) + li;
+        if (hi < H && ho < H) ws[off + (l * H + hi) * H + ho] = dWl[l][o][r];
       }
   off += NH * H * H;
-  // per-row sums over the lane's columns: reduce over li, lane li == 0 writes
+  // per-row sums over the lane's column: reduce over li, then over the two column blocks through LDS
+  float* rowsum = &sm.dz[0][0];  // [2][HP] scratch, free now
   auto put_rows = [&](const float (&v)[4], int dst, int stride) {
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float s = sum16(v[r]);
-      const int h = 16 * w + 4 * lk + r;
-      if (li == 0 && h < H) ws[dst + h * stride] = s;
+      const float sv = sum16(v[r]);
+      if (li == 0) rowsum[cb * HP + L.row(r)] = sv;
     }
+    __syncthreads();
+    if (tid < H) ws[dst + tid * stride] = rowsum[tid] + rowsum[HP + tid];
   };
 #pragma unroll
   for (int l = 0; l < NH; ++l) put_rows(dbl[l], off + l * H, 1);
   off += NH * H;
 #pragma unroll
-  for (int l = 0; l < NH; ++l) put_rows(dgl[l], off + l * H, 1);  // d gamma (x bn scale applied below)
+  for (int l = 0; l < NH; ++l) put_rows(dgl[l], off + l * H, 1);  // d gamma (bn scale applied at scatter)
   off += NH * H;
 #pragma unroll
   for (int l = 0; l < NH; ++l) put_rows(dbe[l], off + l * H, 1);
@@ -669,7 +635,6 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   put_rows(dwh0, off + 0, 2);
   put_rows(dwh1, off + 1, 2);
   off += 2 * H;
-  // b_head: threads 0..31 of wave 0 hold per-position partials
   float s0 = (tid < P) ? dbh0 : 0.f, s1 = (tid < P) ? dbh1 : 0.f;
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
@@ -731,7 +696,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   return a;
 }
 
-}  // namespace flow2
+}  // namespace flow3
 
 // ---------------------------------------------------------------------------
 // entry points used by flow_api.cpp
@@ -739,7 +704,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
 // (HK, KS) buckets: hidden k-steps ceil(H/4) and sample-channel k-steps ceil(k/4), rounded up to
 // the shapes of the reference configs; the generic <NH, 16, 16> covers any H <= 64, k <= 64 (the
 // padded weight images are zero beyond H and k, so extra k-steps add zeros).
-#define FLOW2_CASES(KERNEL, nh, hk, ks, ...)                                                      \
+#define FLOW3_CASES(KERNEL, nh, hk, ks, ...)                                                      \
   do {                                                                                            \
     if (hk == 13 && ks == 2 && nh == 1) hipLaunchKernelGGL((KERNEL<1, 13, 2>), __VA_ARGS__);      \
     else if (hk == 13 && ks == 13 && nh == 1) hipLaunchKernelGGL((KERNEL<1, 13, 13>), __VA_ARGS__); \
@@ -761,59 +726,59 @@ static void buckets(const VissmFlowDesc* d, int* hk, int* ks) {
   if (*hk == 16) *ks = 16;
 }
 
-size_t flow2_workspace_size(const VissmFlowDesc* d, int backward) {
-  using namespace flow2;
+size_t flow3_workspace_size(const VissmFlowDesc* d, int backward) {
+  using namespace flow3;
   Geom g = geom(d, backward != 0);
   return backward ? bwd_ws_layout(d, g, nullptr, nullptr) : fwd_ws_layout(d, g, nullptr, nullptr);
 }
 
-int flow2_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+int flow3_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
               const float* theta_term, float* u_next, float* logsig, void* workspace, size_t ws_bytes,
               hipStream_t st) {
-  using namespace flow2;
+  using namespace flow3;
   Geom g = geom(d, false);
   VISSM_CHECK_ARG(workspace && ws_bytes >= fwd_ws_layout(d, g, nullptr, nullptr), "flow_fwd: workspace too small");
   WsF ws;
   fwd_ws_layout(d, g, reinterpret_cast<char*>(workspace), &ws);
   hipLaunchKernelGGL(prep_kernel, dim3(1), dim3(256), 0, st, *w, d->H, d->k, d->n_hidden, d->bn, ws.w);
-  VISSM_CHECK_LAUNCH("flow2_prep");
+  VISSM_CHECK_LAUNCH("flow3_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid(g.n_groups, g.n_chunks);
   int hk, ks;
   buckets(d, &hk, &ks);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  FLOW2_CASES(fwd_kernel, d->n_hidden, hk, ks, grid, dim3(NT), 0, st, a, u, C, wn, theta_term, ws.w, u_next,
+  FLOW3_CASES(fwd_kernel, d->n_hidden, hk, ks, grid, dim3(NT), 0, st, a, u, C, wn, theta_term, ws.w, u_next,
               ws.ls_slab);
-  VISSM_CHECK_LAUNCH("flow2_fwd");
+  VISSM_CHECK_LAUNCH("flow3_fwd");
   prof_end(VISSM_PROF_FLOW_FWD, st);
   return launch_reduce_rows(ws.ls_slab, logsig, g.n_chunks, d->B, st);
 }
 
-int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+int flow3_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
               const float* theta_term, const float* du_next, const float* dlogsig, float* du, float* dC,
               float* dtheta_term, const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st) {
-  using namespace flow2;
+  using namespace flow3;
   Geom g = geom(d, true);
   VISSM_CHECK_ARG(workspace && ws_bytes >= bwd_ws_layout(d, g, nullptr, nullptr), "flow_bwd: workspace too small");
   WsB ws;
   bwd_ws_layout(d, g, reinterpret_cast<char*>(workspace), &ws);
   hipLaunchKernelGGL(prep_kernel, dim3(1), dim3(256), 0, st, *w, d->H, d->k, d->n_hidden, d->bn, ws.w);
-  VISSM_CHECK_LAUNCH("flow2_prep");
+  VISSM_CHECK_LAUNCH("flow3_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid(g.n_groups, g.n_chunks);
   int hk, ks;
   buckets(d, &hk, &ks);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
-  FLOW2_CASES(bwd_kernel, d->n_hidden, hk, ks, grid, dim3(NT), 0, st, a, u, C, wn, theta_term, du_next, dlogsig, ws.w,
+  FLOW3_CASES(bwd_kernel, d->n_hidden, hk, ks, grid, dim3(NT), 0, st, a, u, C, wn, theta_term, du_next, dlogsig, ws.w,
               du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
-  VISSM_CHECK_LAUNCH("flow2_bwd");
+  VISSM_CHECK_LAUNCH("flow3_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
   if (g.n_chunks > 1) {
     hipLaunchKernelGGL(halo_fixup_kernel, dim3(d->B), dim3(256), 0, st, du, ws.halo, d->B, d->L, d->k, g.n_chunks,
                        g.s, g.CH);
-    VISSM_CHECK_LAUNCH("flow2_halo");
+    VISSM_CHECK_LAUNCH("flow3_halo");
   }
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   int rc;
@@ -824,7 +789,7 @@ int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
     dim3 rg(static_cast<unsigned>((nC + 255) / 256), d->n_win);
     hipLaunchKernelGGL(reduce_by_window_kernel, rg, dim3(256), 0, st, ws.dC_slab, win, dC, d->B,
                        static_cast<int>(nC));
-    VISSM_CHECK_LAUNCH("flow2_reduce_window");
+    VISSM_CHECK_LAUNCH("flow3_reduce_window");
   }
   rc = launch_reduce_rows(ws.dth_slab, dtheta_term, g.n_chunks, static_cast<int64_t>(d->B) * d->H, st);
   if (rc) return rc;
@@ -833,7 +798,7 @@ int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   if (rc) return rc;
   hipLaunchKernelGGL(scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *gr, d->k, d->H,
                      d->n_hidden, d->bn);
-  VISSM_CHECK_LAUNCH("flow2_scatter");
+  VISSM_CHECK_LAUNCH("flow3_scatter");
   return VISSM_OK;
 }
 
