@@ -105,8 +105,9 @@ typedef struct {        /* outputs of the backward: written, not accumulated */
   float* w_head; float* b_head;
 } VissmFlowGrads;
 
-/* Selects the flow implementation for A/B measurements (3 = matrix cores,
- * 8-wave blocks [default]; 2 = matrix cores, 4-wave blocks; 1 = VALU/LDS).
+/* Selects the flow implementation for A/B measurements (4 = matrix cores,
+ * latency-hiding [default]; 3 = matrix cores, 8-wave blocks; 2 = matrix cores,
+ * 4-wave blocks; 1 = VALU/LDS).
  * 0 only queries.  Returns the previous selection. */
 int vissm_flow_set_impl(int32_t which);
 

@@ -1,8 +1,8 @@
 // C-ABI entry points of the IAF flow (include/vissm.h): argument validation and
-// dispatch to the implementation.  flow3 (matrix cores, exact fp32, 8-wave
-// blocks) is the product path; flow2 (4-wave blocks) and flow1 (LDS-tiled VALU
-// fp32) are kept as independent implementations for A/B checks, selected with
-// VISSM_FLOW_IMPL=2 / VISSM_FLOW_IMPL=1.
+// dispatch to the implementation.  flow4 (matrix cores, exact fp32, latency
+// hiding) is the product path; flow3 (8-wave blocks), flow2 (4-wave blocks)
+// and flow1 (LDS-tiled VALU fp32) are kept as independent implementations for
+// A/B checks, selected with VISSM_FLOW_IMPL / vissm_flow_set_impl().
 #include "common.hpp"
 
 #include <cstdlib>
@@ -16,6 +16,11 @@ int flow1_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
 size_t flow3_workspace_size(const VissmFlowDesc* d, int backward);
+size_t flow4_workspace_size(const VissmFlowDesc* d, int backward);
+int flow4_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              float*, float*, void*, size_t, hipStream_t);
+int flow4_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 int flow3_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               float*, float*, void*, size_t, hipStream_t);
 int flow3_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
@@ -30,7 +35,7 @@ static int g_impl = 0;  // 0 = not chosen yet
 static int impl() {
   if (g_impl == 0) {
     const char* e = std::getenv("VISSM_FLOW_IMPL");
-    g_impl = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
+    g_impl = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
   }
   return g_impl;
 }
@@ -56,7 +61,7 @@ using namespace vissm;
 extern "C" {
 
 int vissm_flow_set_impl(int32_t which) {
-  VISSM_CHECK_ARG(which >= 0 && which <= 3, "flow_set_impl: %d not in [0,3]", which);
+  VISSM_CHECK_ARG(which >= 0 && which <= 4, "flow_set_impl: %d not in [0,4]", which);
   const int prev = impl();
   if (which > 0) vissm::g_impl = which;
   return prev;
@@ -67,7 +72,8 @@ size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   switch (impl()) {
     case 1: return flow1_workspace_size(d, backward);
     case 2: return flow2_workspace_size(d, backward);
-    default: return flow3_workspace_size(d, backward);
+    case 3: return flow3_workspace_size(d, backward);
+    default: return flow4_workspace_size(d, backward);
   }
 }
 
@@ -85,7 +91,8 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   switch (impl()) {
     case 1: return flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
     case 2: return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-    default: return flow3_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+    case 3: return flow3_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+    default: return flow4_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
   }
 }
 
@@ -108,7 +115,9 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                              ws_bytes, st);
     case 2: return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
                              ws_bytes, st);
-    default: return flow3_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+    case 3: return flow3_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
+                             ws_bytes, st);
+    default: return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
                               ws_bytes, st);
   }
 }
