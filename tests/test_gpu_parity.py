@@ -40,6 +40,28 @@ def test_ar_parity_multi_window():
     _check(run_parity_case("ar", 6, 50, 10, 3, 32, 3, 10, device=DEV, T=300, starts=starts))
 
 
+# 2-D / BN families: network_dims of 5 layers -> 3 hidden 1x1 layers with BN affine (the papers' shapes)
+@pytest.mark.parametrize("family,B,M,k,nf,H,nl,fw", [
+    ("lv", 4, 24, 4, 2, 16, 5, 3),     # stride-2 head, pair swap between flows, window-length features
+    ("lv", 3, 50, 20, 3, 50, 5, 10),   # paper flow shape (kernel_len 20, 3 flows, [50]*5)
+    ("sv", 4, 24, 6, 2, 16, 5, 3),     # 1-D flows on the log-volatility, observed first coordinate
+    ("sv", 3, 52, 50, 5, 50, 5, 5),    # paper shape (batch_dims 52, kernel_len 50, 5 flows)
+    ("fhn", 4, 24, 4, 2, 16, 5, 3),
+    ("fhn", 3, 50, 20, 3, 50, 5, 10),  # paper shape
+])
+def test_family_parity_single_window(family, B, M, k, nf, H, nl, fw):
+    _check(run_parity_case(family, B, M, k, nf, H, nl, fw, device=DEV))
+
+
+@pytest.mark.parametrize("family,k,T,starts", [
+    ("lv", 6, 160, [0, 40, 80, 80, 120]),
+    ("sv", 8, 160, [0, 40, 120, 40]),
+    ("fhn", 6, 160, [120, 0, 40, 40, 80]),
+])
+def test_family_parity_multi_window(family, k, T, starts):
+    _check(run_parity_case(family, len(starts), 40, k, 2, 24, 5, 3, device=DEV, T=T, starts=starts))
+
+
 def test_ar_deterministic():
     a = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV)
     b = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV)

@@ -209,9 +209,17 @@ __device__ __forceinline__ void kloop(F&& f) {
 }
 
 // per-wave MFMA A-operand weight slices (VGPR-resident when WREG)
+// dcon block pairs (jb, column block): 2 * ceil(4 KS / 16), spread as w, w + 4
+template <int KS>
+struct Pairs {
+  static constexpr int njb = (4 * KS + 15) >> 4;
+  static constexpr int per_wave = (2 * njb + 3) / 4;
+};
+
 template <int HK, int KS, bool WREG>
 struct WRegs {
-  float wf[WREG ? HK : 1], wb[WREG ? HK : 1], we[WREG ? KS : 1], wc[WREG ? HK : 1];
+  float wf[WREG ? HK : 1], wb[WREG ? HK : 1], we[WREG ? KS : 1];
+  float wc[WREG ? Pairs<KS>::per_wave : 1][WREG ? HK : 1];
 };
 
 struct Lane {
@@ -243,10 +251,14 @@ __device__ __forceinline__ void load_wregs(const WImg& W, WRegs<HK, KS, WREG>& R
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) R.we[s] = W.weps[(4 * s + L.lk) * HP + 16 * L.w + L.li];
-    const int pjb = L.w >> 1;
-    if (L.w < 2 * njb) {
 #pragma unroll
-      for (int s = 0; s < HK; ++s) R.wc[s] = W.wepsT[(4 * s + L.lk) * HP + 16 * pjb + L.li];
+    for (int q = 0; q < Pairs<KS>::per_wave; ++q) {
+      const int pair = L.w + 4 * q;
+      const int pjb = pair >> 1;
+      if (pair < 2 * njb) {
+#pragma unroll
+        for (int s = 0; s < HK; ++s) R.wc[q][s] = W.wepsT[(4 * s + L.lk) * HP + 16 * pjb + L.li];
+      }
     }
   }
 }
@@ -668,14 +680,16 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
       for (int jb = 0; jb < njb; ++jb) dWe[jb] = mma(sm.us[a.s * p + 16 * jb + li], bz, dWe[jb]);
     }
-    // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]   (wave w: block pair (jb, cb) = (w >> 1, w & 1))
-    {
-      const int pjb = w >> 1, pcb = w & 1;
-      if (w < 2 * njb) {
+    // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]   (block pairs (jb, cb) = (pair >> 1, pair & 1), pair = w + 4 q)
+#pragma unroll
+    for (int q = 0; q < Pairs<KS>::per_wave; ++q) {
+      const int pair = w + 4 * q;
+      const int pjb = pair >> 1, pcb = pair & 1;
+      if (pair < 2 * njb) {
         f4 dcn = f4{0.f, 0.f, 0.f, 0.f};
         kloop<WREG, HK>([&](int s) {
           const int hh = 4 * s + lk;
-          const float wa = WREG ? R.wc[WREG ? s : 0] : W.wepsT[hh * HP + 16 * pjb + li];
+          const float wa = WREG ? R.wc[WREG ? q : 0][WREG ? s : 0] : W.wepsT[hh * HP + 16 * pjb + li];
           dcn = mma(wa, sm.dz[sw(hh, 16 * pcb + li)], dcn);
         });
         // park dcon [j][p] in act[0]: no wave reads act[0] after the first-layer barrier above

@@ -146,8 +146,7 @@ class VISSMBase:
         out = self.forward(batch, step, eps, x0_theta)
         loss = (-out["elbo"]).sum()
         loss.backward()
-        st.sync_grads()
-        self.dist.all_reduce_(st.grad)
+        self._reduce_grads()
         if apply:
             o = self._opt_main
             gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm())
@@ -157,13 +156,39 @@ class VISSMBase:
     def clip_norm(self) -> float:
         return float(self.grad_clip)
 
+    def grad_mask(self):
+        """Optional 0/1 mask over the flat gradient (frozen variables); None = all trainable."""
+        return None
+
+    def _reduce_grads(self):
+        st = self.store
+        st.sync_grads()
+        m = self.grad_mask()
+        if m is not None:
+            st.grad.mul_(m)
+        self.dist.all_reduce_(st.grad)
+
+    def minimize_pair(self, loss1: torch.Tensor, loss2: torch.Tensor, beta1: float = 0.9, lr: float = 1e-3):
+        """Two AdamaxOptimizer(lr, beta1).minimize ops run in one session step (gradients from the same
+        forward values, each with its own slots): SV pre_train_step + param_init, FHN t1 + t2."""
+        st = self.store
+        st.zero_grad()
+        loss1.backward(retain_graph=True)
+        self._reduce_grads()
+        g1 = st.grad.clone()
+        st.zero_grad()
+        loss2.backward()
+        self._reduce_grads()
+        s1, s2 = self._opt_pre[0], self._opt_pre[1]
+        s1.kernel.step(st.flat, g1, s1.v, s1.m, lr, beta1, 0.999, 1e-8, 0.0)
+        s2.kernel.step(st.flat, st.grad, s2.v, s2.m, lr, beta1, 0.999, 1e-8, 0.0)
+
     def minimize(self, loss: torch.Tensor, slots: AdamaxSlots, beta1: float = 0.9, lr: float = 1e-3):
         """AdamaxOptimizer(learning_rate=lr, beta1).minimize(loss) for a pre-training loss (no clip)."""
         st = self.store
         st.zero_grad()
         loss.backward()
-        st.sync_grads()
-        self.dist.all_reduce_(st.grad)
+        self._reduce_grads()
         slots.kernel.step(st.flat, st.grad, slots.v, slots.m, lr, beta1, 0.999, 1e-8, 0.0)
 
     # model-specific pre-training step; returns True when pre-training is finished
