@@ -85,6 +85,13 @@ def build_model(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_lay
     for name, v in vals.items():
         if name.startswith("theta/") and name.endswith("bias"):
             vals[name] = 0.05 * rng.standard_normal(v.shape)
+    if family == "lv":
+        # LV paths live near the populations (~100); the reference pre-trains lf_sample towards 75
+        # before the ELBO (lotka_volterra_partial.py:301).  Shift mu of the last two flows (between
+        # them every coordinate is transformed once) so the ELBO is finite and well conditioned.
+        nf = model.mdef.n_flows
+        for i in range(max(0, nf - 2), nf):
+            vals[f"flow{i}/head/bias"][0] += 60.0
     model.store.load_numpy(vals)
     model.build_flow()
     return model

@@ -282,7 +282,7 @@ __device__ __forceinline__ void prefetch(const KArgs& a, const float* __restrict
   }
   pf.th = tid < a.H ? tht[static_cast<size_t>(b) * a.H + tid] : 0.f;
   pf.dls = (dls && tid == 0) ? dls[b] : 0.f;
-  pf.win = (win && tid == 0) ? win[b] : 0;
+  pf.win = (win && (tid & 63) == 0) ? win[b] : 0;  // lane 0 of every wave (broadcast by __shfl)
 }
 
 template <int NH>
