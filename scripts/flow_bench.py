@@ -43,17 +43,24 @@ def main():
     bn_g, bn_b = (1 + r(nh, H, sc=0.1), r(nh, H, sc=0.1)) if nh > 1 else (None, None)
     w_head, b_head = r(H, 2, sc=0.2), r(2, sc=0.1)
     gnext, gls = r(B, sh.Lout), r(B)
-    impls = [int(x) for x in (args.only or args.impls).split(",")]
+    # entries: an fp32 implementation number (1-4) or "bf16" / "bf16x3" (matrix-core bf16 kernels)
+    PREC = {"bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}
+    impls = [x if x in PREC else int(x) for x in (args.only or args.impls).split(",")]
+    import dataclasses
     res = {}
     outs = {}
     for rd in range(args.rounds):
         for im in impls:
-            lib.vissm_flow_set_impl(im)
+            shp = sh
+            if im in PREC:
+                shp = dataclasses.replace(sh, precision=PREC[im])
+            else:
+                lib.vissm_flow_set_impl(im)
             ins = [t.clone().requires_grad_(True) for t in (u, C, tt, w_eps, w_hid, b_hid, w_head, b_head)]
             extra = [bn_g, bn_b]
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            un, ls = MAFlowFn.apply(sh, None, ins[0], ins[1], ins[2], ins[3], ins[4], ins[5], extra[0], extra[1],
+            un, ls = MAFlowFn.apply(shp, None, ins[0], ins[1], ins[2], ins[3], ins[4], ins[5], extra[0], extra[1],
                                     ins[6], ins[7])
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -69,11 +76,13 @@ def main():
         b = sorted(x[1] for x in v[1:] or v)
         summary[im] = {"fwd_ms": 1e3 * f[len(f) // 2], "bwd_ms": 1e3 * b[len(b) // 2]}
     if len(outs) > 1:
-        ks = sorted(outs)
+        ks = sorted(outs, key=str)
         a0 = outs[ks[0]]
+        names = ["u_next", "logsig", "du", "dC", "dtheta", "dw_eps", "dw_hid", "db_hid", "dw_head", "db_head"]
         for im in ks[1:]:
             errs = [float((x - y).norm() / (y.norm() + 1e-30)) for x, y in zip(outs[im], a0)]
-            summary[im]["max_rel_diff_vs_%d" % ks[0]] = max(errs)
+            summary[im]["max_rel_diff_vs_%s" % ks[0]] = max(errs)
+            summary[im]["rel_diff"] = dict(zip(names, errs))
     print(json.dumps({"shape": vars(args), "results": summary}))
 
 

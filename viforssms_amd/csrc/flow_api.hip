@@ -30,6 +30,13 @@ int flow2_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 int flow2_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 
+bool flow5_supports(const VissmFlowDesc* d);
+size_t flow5_workspace_size(const VissmFlowDesc* d, int backward);
+int flow5_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              float*, float*, void*, size_t, hipStream_t);
+int flow5_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
+              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
+
 static int g_impl = 0;  // 0 = not chosen yet
 
 static int impl() {
@@ -50,9 +57,16 @@ static int validate(const VissmFlowDesc* d) {
   VISSM_CHECK_ARG(!d->swap_out || ((d->L - d->k) % 2 == 0), "flow: swap_out needs an even output length");
   VISSM_CHECK_ARG(d->n_logsig >= 0 && d->n_logsig <= d->L - d->k, "flow: bad n_logsig");
   VISSM_CHECK_ARG(d->n_win >= 1, "flow: n_win must be >= 1");
-  VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32, "flow: precision %d not supported by this build", d->precision);
+  VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32 || d->precision == VISSM_PREC_BF16 ||
+                      d->precision == VISSM_PREC_BF16X3,
+                  "flow: unknown precision %d", d->precision);
   return VISSM_OK;
 }
+
+// bf16 / bf16x3 requests run on the bf16 matrix-core kernels (flow_v5) where they
+// cover the shape; anything else runs the exact-fp32 kernels (never less precise
+// than requested).
+static bool use_v5(const VissmFlowDesc* d) { return d->precision != VISSM_PREC_FP32 && flow5_supports(d); }
 
 }  // namespace vissm
 
@@ -69,6 +83,7 @@ int vissm_flow_set_impl(int32_t which) {
 
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
+  if (use_v5(d)) return flow5_workspace_size(d, backward);
   switch (impl()) {
     case 1: return flow1_workspace_size(d, backward);
     case 2: return flow2_workspace_size(d, backward);
@@ -88,6 +103,7 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (w->bn_g && w->bn_b), "flow_fwd: bn needs bn_g/bn_b");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
+  if (use_v5(d)) return flow5_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
   switch (impl()) {
     case 1: return flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
     case 2: return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
@@ -110,6 +126,8 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                   "flow_bwd: bn needs bn_g/bn_b pointers");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
+  if (use_v5(d))
+    return flow5_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
   switch (impl()) {
     case 1: return flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
                              ws_bytes, st);
