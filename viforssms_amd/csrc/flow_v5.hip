@@ -1,100 +1,137 @@
-// IAF flow of the neural-MA sampler on the bf16 matrix cores
-// (v_mfma_f32_16x16x32_bf16, fp32 accumulation): forward and backward.
+// IAF flow of the neural-MA sampler on the bf16 matrix cores (fp32 accumulation):
+// forward and backward.
 //
-// Precision: VISSM_PREC_BF16 (one product per MFMA: bf16 operands) or
-// VISSM_PREC_BF16X3 (split operands a = a_hi + a_lo, three products
-// a_hi b_hi + a_hi b_lo + a_lo b_hi: ~2^-16 relative per product).
+// Precision: VISSM_PREC_BF16 (bf16 operands, one product per MFMA) or
+// VISSM_PREC_BF16X3 (split operands a = a_hi + a_lo, products a_hi b_hi + a_hi b_lo
+// + a_lo b_hi: ~2^-16 relative per product, fp32-class results).
 //
 // Reference: IAF._create_flow / IAF.slp (AR.py:50-89), stride-2 head
 // (lotka_volterra_partial.py:97-104), Permute fused into the store (swap_out).
 //
-// Design (wave-centric, no block barriers on the step path):
-//   * a work unit = one (sample, tile of P = 32 head positions) is processed by
-//     ONE wave; a block's 4 waves run independent work items and share only the
-//     weight fragments staged in LDS once per block;
-//   * activations are MFMA accumulators X[rb][cb] (lane (g, c) holds rows
-//     h = 16 rb + 4 g + r, column p = 16 cb + c).  Products that contract over h
-//     (forward layers, head, dX = W dZ, dcon = w_eps dA0) take the accumulators
-//     directly as the B operand: k-step ks packs rows 32 ks + 16 (j >> 2) + 4 g
-//     + (j & 3) of the lane's own registers, and the weight fragments in LDS are
-//     pre-permuted to the same k order (hperm below) -- no LDS round trip, no
-//     lane movement;
+// Design (wave-centric: no block barriers on the step path):
+//   * a work unit = one (sample, tile of P = 16 head positions) is processed by ONE
+//     wave; a block's 4 waves run independent work items and share only the weight
+//     fragments staged in LDS once per block;
+//   * activations are MFMA accumulators X[rb] (lane (g, c) holds rows
+//     h = 16 rb + 4 g + r, position p = c).  Products that contract over h (hidden
+//     layer, head, dX = W dZ, dcon = w_eps dA0, the dC identity-selection) take the
+//     accumulators directly as the B operand of v_mfma_f32_16x16x32_bf16: k-step ks
+//     packs rows 32 ks + 16 (j >> 2) + 4 g + (j & 3) of the lane's own registers and
+//     the weight fragments are pre-permuted to that k order (hperm) -- no LDS round
+//     trip, no lane movement;
 //   * products that contract over positions (dW = X dZ^T, dW_eps = U dA0^T,
-//     d theta = dA0 1) need h on the lane: the wave writes the bf16 tile into a
-//     private swizzled [p][h] LDS image (8-byte stores) and reads it back
-//     transposed with ds_read_b64_tr_b16;
-//   * bias gradients come free from a row of ones in the padded activations
-//     (row 63 of X_l: W is zero there, so the forward is unchanged and
-//     dW[63][:] accumulates sum_p dZ);
-//   * grid decomposition, carries, halo and fixed-order partial slabs are those
-//     of flow_v4.hip (sample groups x t-chunks; backward walks tiles outer /
-//     samples inner so the window-shared dC tile is summed over the group in
-//     registers).
-// Supported here: n_hidden <= 1 without BN, H <= 63, k <= 64 (the AR
-// configurations); other shapes are served by flow_v4 (fp32).
+//     d theta = dA0 1, dW_head = X1 G^T) use v_mfma_f32_16x16x16_bf16 on fragments
+//     read from a wave-private swizzled [p][h] LDS image with ds_read_b64_tr_b16
+//     (one read per fragment);
+//   * bias gradients come free from a row of ones in the padded activations (row 63:
+//     W is zero there, so the forward is unchanged and dW[63][:] = sum_p dZ);
+//   * grid decomposition, carries, halo and fixed-order partial slabs follow
+//     flow_v4.hip (sample groups x t-chunks; the backward walks tiles outer / samples
+//     inner so the window-shared dC tile is summed over the group in accumulators).
+// Supported: n_hidden = 1 without BN, H <= 63, k <= 64 (the AR configurations);
+// other shapes run on flow_v4 (exact fp32).
 #include "common.hpp"
 
 namespace vissm {
 namespace flow5 {
 
-constexpr int P = 32;
+constexpr int P = 16;
 constexpr int HP = 64;
 constexpr int S = 16;
 constexpr int NW = 4;
 constexpr int NT = 64 * NW;
+constexpr int UW = 128;  // u window staged per unit: s * P + k <= 96
 
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf4 lds_bf4;
 
+// fragments: hi (and lo for NP == 3)
 template <int NP>
-struct Fr {
-  bf8 h, l;  // l used only when NP == 3
+struct Fr8 {
+  bf8 h, l;
+};
+template <int NP>
+struct Fr4 {
+  bf4 h, l;
 };
 
-__device__ __forceinline__ f4 mfma(bf8 a, bf8 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f4 mfma32(bf8 a, bf8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f4 mfma16(bf4 a, bf4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a), __builtin_bit_cast(s4, b), c, 0, 0, 0);
 }
 
 template <int NP>
-__device__ __forceinline__ f4 mm(const Fr<NP>& a, const Fr<NP>& b, f4 c) {
+__device__ __forceinline__ f4 mm(const Fr8<NP>& a, const Fr8<NP>& b, f4 c) {
   if constexpr (NP == 3) {
-    c = mfma(a.l, b.h, c);
-    c = mfma(a.h, b.l, c);
+    c = mfma32(a.l, b.h, c);
+    c = mfma32(a.h, b.l, c);
   }
-  return mfma(a.h, b.h, c);
+  return mfma32(a.h, b.h, c);
+}
+template <int NP>
+__device__ __forceinline__ f4 mm(const Fr4<NP>& a, const Fr4<NP>& b, f4 c) {
+  if constexpr (NP == 3) {
+    c = mfma16(a.l, b.h, c);
+    c = mfma16(a.h, b.l, c);
+  }
+  return mfma16(a.h, b.h, c);
+}
+// one operand exact in bf16 (ones / selections)
+template <int NP>
+__device__ __forceinline__ f4 mm_ax(bf8 a, const Fr8<NP>& b, f4 c) {
+  if constexpr (NP == 3) c = mfma32(a, b.l, c);
+  return mfma32(a, b.h, c);
+}
+template <int NP>
+__device__ __forceinline__ f4 mm_bx(const Fr4<NP>& a, bf4 b, f4 c) {
+  if constexpr (NP == 3) c = mfma16(a.l, b, c);
+  return mfma16(a.h, b, c);
 }
 
-// b exact in bf16 (ones)
-template <int NP>
-__device__ __forceinline__ f4 mm_bexact(const Fr<NP>& a, bf8 b, f4 c) {
-  if constexpr (NP == 3) c = mfma(a.l, b, c);
-  return mfma(a.h, b, c);
+__device__ __forceinline__ unsigned cvt2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, bf2));
+}
+__device__ __forceinline__ float lo_of(float x, unsigned packed, int half) {
+  // x - float(bf16 half of packed)
+  const unsigned bits = half ? (packed & 0xffff0000u) : (packed << 16);
+  return x - __builtin_bit_cast(float, bits);
 }
 
 template <int NP>
-__device__ __forceinline__ Fr<NP> split8(const float (&v)[8]) {
-  Fr<NP> f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
-    f.h[j] = h;
-    if constexpr (NP == 3) f.l[j] = (__bf16)(v[j] - (float)h);
+__device__ __forceinline__ Fr8<NP> split8(const f4& x0, const f4& x1) {
+  Fr8<NP> f;
+  const u4 h = {cvt2(x0[0], x0[1]), cvt2(x0[2], x0[3]), cvt2(x1[0], x1[1]), cvt2(x1[2], x1[3])};
+  f.h = __builtin_bit_cast(bf8, h);
+  if constexpr (NP == 3) {
+    const u4 l = {cvt2(lo_of(x0[0], h[0], 0), lo_of(x0[1], h[0], 1)), cvt2(lo_of(x0[2], h[1], 0), lo_of(x0[3], h[1], 1)),
+                  cvt2(lo_of(x1[0], h[2], 0), lo_of(x1[1], h[2], 1)), cvt2(lo_of(x1[2], h[3], 0), lo_of(x1[3], h[3], 1))};
+    f.l = __builtin_bit_cast(bf8, l);
+  }
+  return f;
+}
+template <int NP>
+__device__ __forceinline__ Fr4<NP> split4(const f4& x) {
+  Fr4<NP> f;
+  const u2 h = {cvt2(x[0], x[1]), cvt2(x[2], x[3])};
+  f.h = __builtin_bit_cast(bf4, h);
+  if constexpr (NP == 3) {
+    const u2 l = {cvt2(lo_of(x[0], h[0], 0), lo_of(x[1], h[0], 1)), cvt2(lo_of(x[2], h[1], 0), lo_of(x[3], h[1], 1))};
+    f.l = __builtin_bit_cast(bf4, l);
   }
   return f;
 }
 
-// chain B fragment: k-step ks of activations X (rows 32ks .. 32ks+31), column block cb
+// chain B fragment of activations X (one column block): k-step ks = rows 32ks .. 32ks + 31
 template <int NP>
-__device__ __forceinline__ Fr<NP> chain_frag(const f4 (&X)[4][2], int ks, int cb) {
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = X[2 * ks][cb][j];
-    v[4 + j] = X[2 * ks + 1][cb][j];
-  }
-  return split8<NP>(v);
+__device__ __forceinline__ Fr8<NP> chain_frag(const f4 (&X)[4], int ks) {
+  return split8<NP>(X[2 * ks], X[2 * ks + 1]);
 }
 
 // hidden row of element j of k-step ks in lane group g (the chain k order)
@@ -102,21 +139,25 @@ __host__ __device__ __forceinline__ int hperm(int ks, int g, int j) {
   return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
 }
 
+__device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+__device__ __forceinline__ float elu_d(float y) { return y < 0.f ? y + 1.f : 1.f; }
+
 // ---------------------------------------------------------------------------
-// weight fragments: [frag][plane (hi, lo)][lane] of 8 bf16, index layout
-//   WF(l, ob, ks)  l*8 + ob*2 + ks             forward hidden   A[h_out][h_in perm]
-//   WB(l, ib, ks)  8*NH + l*8 + ib*2 + ks      dX = W dZ        A[h_in][h_out perm]
-//   WE(kb, ob)     16*NH + kb*4 + ob           layer 0          A[h][j]
-//   WC(jb, ks)     16*NH + 4*KB + jb*2 + ks    dcon             A[j][h perm]
-//   WH(ks)         16*NH + 4*KB + 2*JB + ks    head             A[o][h perm]
+// weight fragments (8 bf16 per lane): [frag][plane (hi, lo)][lane]
+//   WF(ob, ks)   ob*2 + ks          forward hidden    A[h_out][h_in perm]
+//   WB(ib, ks)   8 + ib*2 + ks      dX = W dZ         A[h_in][h_out perm]
+//   WE(kb, ob)   16 + kb*4 + ob     layer 0           A[h][j]
+//   WC(jb, ks)   16 + 4KB + jb*2+ks dcon              A[j][h perm]
+//   WH(ks)       16 + 4KB + 2JB+ks  head              A[o][h perm]
+//   IS(ob)       18 + 4KB + 2JB+ob  dC selection      A[h][h perm] = identity (exact; hi plane only)
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * NH + 4 * KB + 2 * JB + 2; }
+__host__ __device__ constexpr int n_frags(int KB, int JB) { return 16 + 4 * KB + 2 * JB + 2 + 4; }
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
 };
 
-__global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int NP, int KB, int JB, bf8* __restrict__ img,
+__global__ void prep_kernel(VissmFlowParams w, int H, int k, int NP, int KB, int JB, bf8* __restrict__ img,
                             float* __restrict__ cst) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   const int NPL = NP == 3 ? 2 : 1;
@@ -124,15 +165,15 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int NP, int
   for (int j = 0; j < 8; ++j) {
     float x = 0.f;
     int r = f;
-    if (r < 8 * nh) {  // WF
-      const int l = r >> 3, ob = (r >> 1) & 3, ks = r & 1;
+    if (r < 8) {  // WF
+      const int ob = r >> 1, ks = r & 1;
       const int hin = hperm(ks, g, j), hout = 16 * ob + c;
-      if (hin < H && hout < H) x = w.w_hid[(static_cast<size_t>(l) * H + hin) * H + hout];
-    } else if ((r -= 8 * nh) < 8 * nh) {  // WB
-      const int l = r >> 3, ib = (r >> 1) & 3, ks = r & 1;
+      if (hin < H && hout < H) x = w.w_hid[hin * H + hout];
+    } else if ((r -= 8) < 8) {  // WB
+      const int ib = r >> 1, ks = r & 1;
       const int hin = 16 * ib + c, hout = hperm(ks, g, j);
-      if (hin < H && hout < H) x = w.w_hid[(static_cast<size_t>(l) * H + hin) * H + hout];
-    } else if ((r -= 8 * nh) < 4 * KB) {  // WE
+      if (hin < H && hout < H) x = w.w_hid[hin * H + hout];
+    } else if ((r -= 8) < 4 * KB) {  // WE
       const int kb = r >> 2, ob = r & 3;
       const int jt = 32 * kb + 8 * g + j, h = 16 * ob + c;
       if (jt < k && h < H) x = w.w_eps[jt * H + h];
@@ -140,10 +181,12 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int NP, int
       const int jb = r >> 1, ks = r & 1;
       const int jt = 16 * jb + c, h = hperm(ks, g, j);
       if (jt < k && h < H) x = w.w_eps[jt * H + h];
-    } else {  // WH
-      const int ks = r - 2 * JB;
-      const int h = hperm(ks, g, j);
+    } else if ((r -= 2 * JB) < 2) {  // WH
+      const int h = hperm(r, g, j);
       if (c < 2 && h < H) x = w.w_head[h * 2 + c];
+    } else {  // IS
+      const int ob = r - 2;
+      x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
     }
     v[j] = x;
   }
@@ -155,225 +198,192 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int NP, int
   img[(f * NPL + 0) * 64 + lane] = hi;
   if (NPL == 2) img[(f * NPL + 1) * 64 + lane] = lo;
   if (f == 0) {
-    // constants: bias[nh][64], w_head[2][64], b_head[2]
-    for (int l = 0; l < nh; ++l) cst[l * HP + lane] = lane < H ? w.b_hid[l * H + lane] : 0.f;
-    cst[nh * HP + lane] = lane < H ? w.w_head[lane * 2 + 0] : 0.f;
-    cst[nh * HP + HP + lane] = lane < H ? w.w_head[lane * 2 + 1] : 0.f;
-    if (lane < 2) cst[nh * HP + 2 * HP + lane] = w.b_head[lane];
+    // constants: bias[64], w_head[2][64], b_head[2]
+    cst[lane] = lane < H ? w.b_hid[lane] : 0.f;
+    cst[HP + lane] = lane < H ? w.w_head[lane * 2 + 0] : 0.f;
+    cst[2 * HP + lane] = lane < H ? w.w_head[lane * 2 + 1] : 0.f;
+    if (lane < 2) cst[3 * HP + lane] = w.b_head[lane];
   }
 }
 
-// ---------------------------------------------------------------------------
-// per-block LDS
-// ---------------------------------------------------------------------------
-template <int NH, int KB, int JB, int NP>
+// zero-padded 64-wide copies of C [n_win][Lh][H] and of the theta term [B][H]
+__global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t rows, int H) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= rows * HP) return;
+  const int64_t r = i / HP;
+  const int h = static_cast<int>(i % HP);
+  dst[i] = h < H ? src[r * H + h] : 0.f;
+}
+
+template <int KB, int JB, int NP>
 struct Shared {
-  static constexpr int NFR = n_frags(NH, KB, JB);
+  static constexpr int NFR = n_frags(KB, JB);
   static constexpr int NPL = NP == 3 ? 2 : 1;
   bf8 img[NFR][NPL][64];
-  float cst[(NH + 2) * HP + 4];
+  float cst[3 * HP + 4];
 };
 
-// transposed-image addressing: [p][h] bf16, 16 chunks of 4 per 128-byte row, chunk XOR (row & 15)
-__device__ __forceinline__ int timg_off(int p, int ch) { return p * HP + 4 * (ch ^ (p & 15)); }
-
-template <int NP>
-struct Img {
-  __bf16* plane[NP == 3 ? 2 : 1];
-};
-
-// store a [64 h][32 p] activation tile (normal accumulator layout) into a transposed image
-template <int NP>
-__device__ __forceinline__ void put_image(__bf16* hi, __bf16* lo, const f4 (&X)[4][2], int g, int c) {
-#pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      bf4 h4, l4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const __bf16 hh = (__bf16)X[rb][cb][r];
-        h4[r] = hh;
-        if constexpr (NP == 3) l4[r] = (__bf16)(X[rb][cb][r] - (float)hh);
-      }
-      const int off = timg_off(16 * cb + c, 4 * rb + g);
-      *reinterpret_cast<bf4*>(hi + off) = h4;
-      if constexpr (NP == 3) *reinterpret_cast<bf4*>(lo + off) = l4;
-    }
-}
-
-// a lane's own entries of an image it wrote (normal layout), as fp32 (hi + lo)
-template <int NP>
-__device__ __forceinline__ f4 get_own(const __bf16* hi, const __bf16* lo, int rb, int cb, int g, int c) {
-  const int off = timg_off(16 * cb + c, 4 * rb + g);
-  const bf4 h4 = *reinterpret_cast<const bf4*>(hi + off);
-  f4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = (float)h4[i];
-  if constexpr (NP == 3) {
-    const bf4 l4 = *reinterpret_cast<const bf4*>(lo + off);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] += (float)l4[i];
-  }
-  return r;
-}
-
-__device__ __forceinline__ bf8 tr_read(const __bf16* img, int hb, int g, int c) {
-  const int q = c >> 2, pp = c & 3;
-  const int r0 = 8 * g + q, r1 = 8 * g + 4 + q;
-  const int ch = 4 * hb + pp;
-  bf4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)(img + timg_off(r0, ch)));
-  bf4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)(img + timg_off(r1, ch)));
-  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-template <int NP>
-__device__ __forceinline__ Fr<NP> tr_frag(const __bf16* hi, const __bf16* lo, int hb, int g, int c) {
-  Fr<NP> f;
-  f.h = tr_read(hi, hb, g, c);
-  if constexpr (NP == 3) f.l = tr_read(lo, hb, g, c);
-  return f;
-}
-
-// Compiler-only fence: the weight fragments are loop-invariant LDS loads; without it the
-// compiler hoists all of them out of the unit loop and keeps ~100-200 VGPRs live.
+// Compiler-only fence: keeps the (loop-invariant) LDS weight-fragment loads next to their
+// use instead of hoisted out of the unit loop with ~100-200 VGPRs live.
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
 
-template <int NH, int KB, int JB, int NP>
-__device__ __forceinline__ Fr<NP> wfrag(const Shared<NH, KB, JB, NP>& sh, int f, int lane) {
-  Fr<NP> r;
+template <int KB, int JB, int NP>
+__device__ __forceinline__ Fr8<NP> wfrag(const Shared<KB, JB, NP>& sh, int f, int lane) {
+  Fr8<NP> r;
   r.h = sh.img[f][0][lane];
   if constexpr (NP == 3) r.l = sh.img[f][1][lane];
   return r;
 }
 
-template <int NH, int KB, int JB, int NP>
-__device__ __forceinline__ void load_shared(Shared<NH, KB, JB, NP>& sh, const bf8* __restrict__ img,
+template <int KB, int JB, int NP>
+__device__ __forceinline__ void load_shared(Shared<KB, JB, NP>& sh, const bf8* __restrict__ img,
                                             const float* __restrict__ cst) {
-  constexpr int N = Shared<NH, KB, JB, NP>::NFR * Shared<NH, KB, JB, NP>::NPL * 64;
+  constexpr int N = Shared<KB, JB, NP>::NFR * Shared<KB, JB, NP>::NPL * 64;
   for (int i = threadIdx.x; i < N; i += NT) (&sh.img[0][0][0])[i] = img[i];
-  for (int i = threadIdx.x; i < (NH + 2) * HP + 4; i += NT) sh.cst[i] = cst[i];
+  for (int i = threadIdx.x; i < 3 * HP + 4; i += NT) sh.cst[i] = cst[i];
 }
 
-__device__ __forceinline__ float ld_guard(const float* __restrict__ p, int i, int n) { return i < n ? p[i] : 0.f; }
+// transposed image: [p = 16 rows][64 h] bf16, 16 chunks of 4 per 128-byte row, chunk XOR row
+__device__ __forceinline__ int timg_off(int p, int ch) { return p * HP + 4 * (ch ^ p); }
 
-// layer-0 B fragment: U[j = 32 kb + 8 g + jj][p = 16 cb + c] = u[t0 + s p + j]
 template <int NP>
-__device__ __forceinline__ Fr<NP> u_frag(const float* __restrict__ ub, int L, int k, int t0, int s, int kb, int cb,
-                                         int g, int c) {
-  float v[8];
-  const int j0 = 32 * kb + 8 * g;
-  const int base = t0 + s * (16 * cb + c) + j0;
+__device__ __forceinline__ void put_image(__bf16* hi, __bf16* lo, const f4 (&X)[4], int g, int c) {
 #pragma unroll
-  for (int jj = 0; jj < 8; ++jj) v[jj] = (j0 + jj < k) ? ld_guard(ub, base + jj, L) : 0.f;
-  return split8<NP>(v);
-}
-
-// dW_eps A fragment: U[j = 16 jb + c][p = 8 g + jj] = u[t0 + s p + j]
-template <int NP>
-__device__ __forceinline__ Fr<NP> ua_frag(const float* __restrict__ ub, int L, int k, int t0, int s, int jb, int nP,
-                                          int g, int c) {
-  float v[8];
-  const int j = 16 * jb + c;
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) {
-    const int p = 8 * g + jj;
-    v[jj] = (j < k && p < nP) ? ld_guard(ub, t0 + s * p + j, L) : 0.f;
+  for (int rb = 0; rb < 4; ++rb) {
+    const u2 h = {cvt2(X[rb][0], X[rb][1]), cvt2(X[rb][2], X[rb][3])};
+    const int off = timg_off(c, 4 * rb + g);
+    *reinterpret_cast<u2*>(hi + off) = h;
+    if constexpr (NP == 3) {
+      const u2 l = {cvt2(lo_of(X[rb][0], h[0], 0), lo_of(X[rb][1], h[0], 1)),
+                    cvt2(lo_of(X[rb][2], h[1], 0), lo_of(X[rb][3], h[1], 1))};
+      *reinterpret_cast<u2*>(lo + off) = l;
+    }
   }
-  return split8<NP>(v);
 }
 
-// forward of one unit; on return X[l] (l = 0..NH) hold the layer outputs (row 63 of X[l < NH]
-// set to 1 for the bias-gradient trick) and mu/r the head outputs of this lane's columns.
-template <int NH, int KB, int JB, int NP>
-__device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB, JB, NP>& sh,
-                                             const float* __restrict__ ub, const float* __restrict__ Cw,
-                                             const float* __restrict__ thb, int m0, int nP, int t0,
-                                             f4 (&X)[NH + 1][4][2], float (&mu)[2], float (&rr)[2]) {
+// a lane's own entries of an image it wrote, as fp32 (hi + lo)
+template <int NP>
+__device__ __forceinline__ f4 get_own(const __bf16* hi, const __bf16* lo, int rb, int g, int c) {
+  const int off = timg_off(c, 4 * rb + g);
+  const u2 h = *reinterpret_cast<const u2*>(hi + off);
+  f4 r = {__builtin_bit_cast(float, h[0] << 16), __builtin_bit_cast(float, h[0] & 0xffff0000u),
+          __builtin_bit_cast(float, h[1] << 16), __builtin_bit_cast(float, h[1] & 0xffff0000u)};
+  if constexpr (NP == 3) {
+    const u2 l = *reinterpret_cast<const u2*>(lo + off);
+    r += f4{__builtin_bit_cast(float, l[0] << 16), __builtin_bit_cast(float, l[0] & 0xffff0000u),
+            __builtin_bit_cast(float, l[1] << 16), __builtin_bit_cast(float, l[1] & 0xffff0000u)};
+  }
+  return r;
+}
+
+// K = 16 fragment over positions: lane (g, c) receives X[h = 16 hb + c][p = 4 g + jj], jj = 0..3
+__device__ __forceinline__ bf4 tr_read(const __bf16* img, int hb, int g, int c) {
+  const int row = 4 * g + (c >> 2), ch = 4 * hb + (c & 3);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)(img + timg_off(row, ch)));
+}
+template <int NP>
+__device__ __forceinline__ Fr4<NP> tr_frag(const __bf16* hi, const __bf16* lo, int hb, int g, int c) {
+  Fr4<NP> f;
+  f.h = tr_read(hi, hb, g, c);
+  if constexpr (NP == 3) f.l = tr_read(lo, hb, g, c);
+  return f;
+}
+
+__device__ __forceinline__ int clampi(int i, int n) { return i < n ? i : n - 1; }
+
+// Per-unit inputs, loaded branch-free at the top of the unit: the u window [t0, t0 + 128) and
+// (backward) the upstream-gradient window [t0, t0 + 64) staged in the wave's LDS; C + theta
+// term for the lane's 16 (h, p = c) entries from the zero-padded 64-wide copies (pad_kernel).
+__device__ __forceinline__ void load_unit(const KArgs& a, const float* __restrict__ ub, const float* __restrict__ gb,
+                                          const float* __restrict__ Cw, const float* __restrict__ thb, int m0, int nP,
+                                          int t0, float* uw, float* gw, f4 (&cin)[4]) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  // accumulator init: C^T + theta term
-  float th[4][4];
+  const float u0 = ub[clampi(t0 + lane, a.L)];
+  const float u1 = ub[clampi(t0 + 64 + lane, a.L)];
+  float gv = 0.f;
+  if (gb) {
+    const int o = t0 + lane;
+    gv = gb[clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
+  }
+  const f4* crow = reinterpret_cast<const f4*>(Cw + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
+  const f4* trow = reinterpret_cast<const f4*>(thb) + g;
+  const float pv = c < nP ? 1.f : 0.f;
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < 4; ++rb) cin[rb] = (crow[4 * rb] + trow[4 * rb]) * pv;
+  uw[lane] = u0;
+  uw[64 + lane] = u1;
+  if (gb) gw[lane] = gv;
+}
+
+// layer-0 B fragment: U[j = 32 kb + 8 g + jj][p = c] = u[t0 + s c + j] (weights are zero for j >= k)
+template <int NP>
+__device__ __forceinline__ Fr8<NP> u_frag(const float* uw, int s, int kb, int g, int c) {
+  const float* q = uw + s * c + 32 * kb + 8 * g;
+  return split8<NP>(f4{q[0], q[1], q[2], q[3]}, f4{q[4], q[5], q[6], q[7]});
+}
+
+// dW_eps A fragment (K = 16 positions): U[j = 16 jb + c][p = 4 g + jj] = u[t0 + s p + j]
+// (rows j >= k are discarded; positions p >= nP meet dA0 = 0)
+template <int NP>
+__device__ __forceinline__ Fr4<NP> ua_frag(const float* uw, int s, int jb, int g, int c) {
+  const float* q = uw + s * 4 * g + 16 * jb + c;
+  return split4<NP>(f4{q[0], q[s], q[2 * s], q[3 * s]});
+}
+
+// forward of one unit from its staged inputs; X[0] holds C + theta on entry.  On return
+// X[0], X[1] hold the layer outputs and mu / rr the head outputs at p = c.
+template <int KB, int JB, int NP>
+__device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<KB, JB, NP>& sh, const float* uw,
+                                             f4 (&X)[2][4], float& mu, float& rr) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  f4 acc[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = 16 * rb + 4 * g + r;
-      th[rb][r] = h < a.H ? thb[h] : 0.f;
-    }
+  for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int p = 16 * cb + c;
-    const bool pv = p < nP;
-    const float* crow = Cw + static_cast<size_t>(m0 + p) * a.H;
+  for (int kb = 0; kb < KB; ++kb) {
+    const Fr8<NP> uf = u_frag<NP>(uw, a.s, kb, g, c);
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int h = 16 * rb + 4 * g + r;
-        X[0][rb][cb][r] = (pv && h < a.H) ? crow[h] + th[rb][r] : 0.f;
-      }
+    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, 16 + kb * 4 + ob, lane), uf, acc[ob]);
   }
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const Fr<NP> uf = u_frag<NP>(ub, a.L, a.k, t0, a.s, kb, cb, g, c);
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) X[0][ob][cb] = mm<NP>(wfrag(sh, 16 * NH + kb * 4 + ob, lane), uf, X[0][ob][cb]);
-    }
-#pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+    for (int r = 0; r < 4; ++r) X[0][rb][r] = elu_fast(acc[rb][r] + X[0][rb][r]);
+  fence();
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[0][rb][cb][r] = elu_f(X[0][rb][cb][r]);
+  for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int l = 0; l < NH; ++l) {
-    fence();
-    f4 Z[4][2];
+  for (int ks = 0; ks < 2; ++ks) {
+    const Fr8<NP> xf = chain_frag<NP>(X[0], ks);
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[l * HP + 16 * ob + 4 * g]);
-      Z[ob][0] = bv;
-      Z[ob][1] = bv;
-    }
+    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, ob * 2 + ks, lane), xf, acc[ob]);
+  }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+  for (int rb = 0; rb < 4; ++rb) {
+    const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[16 * rb + 4 * g]);
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const Fr<NP> xf = chain_frag<NP>(X[l], ks, cb);
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob) Z[ob][cb] = mm<NP>(wfrag(sh, l * 8 + ob * 2 + ks, lane), xf, Z[ob][cb]);
-      }
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) X[l + 1][rb][cb][r] = elu_f(Z[rb][cb][r]);
+    for (int r = 0; r < 4; ++r) X[1][rb][r] = elu_fast(acc[rb][r] + bv[r]);
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus)
   fence();
-  const int fh = 16 * NH + 4 * KB + 2 * JB;
+  const int fh = 16 + 4 * KB + 2 * JB;
+  f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    f4 d = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X[NH], ks, cb), d);
-    mu[cb] = __shfl(d[0], c, 64) + sh.cst[NH * HP + 2 * HP + 0];
-    rr[cb] = __shfl(d[1], c, 64) + sh.cst[NH * HP + 2 * HP + 1];
-  }
+  for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X[1], ks), d);
+  mu = __shfl(d[0], c, 64) + sh.cst[3 * HP + 0];
+  rr = __shfl(d[1], c, 64) + sh.cst[3 * HP + 1];
 }
 
 // ---------------------------------------------------------------------------
 // forward kernel: one work item (sample group x t-chunk) per wave; samples outer
 // ---------------------------------------------------------------------------
-template <int NH, int KB, int JB, int NP>
+template <int KB, int JB, int NP>
 __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ u_next, float* __restrict__ ls_slab) {
-  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ Shared<KB, JB, NP> sh;
+  __shared__ float uwin[NW][UW];
   load_shared(sh, img, cst);
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -382,34 +392,31 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
   const int grp = item / a.n_chunks, ch = item % a.n_chunks;
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
+  float* uw = uwin[w];
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     const float* ub = u + static_cast<size_t>(b) * a.L;
     float* ob = u_next + static_cast<size_t>(b) * a.Lout;
     const int wi = win ? win[b] : 0;
-    const float* Cw = C + static_cast<size_t>(wi) * a.Lh * a.H;
+    const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
     float ls = 0.f;
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
       fence();
       const int nP = min(P, m_hi - m0), t0 = a.s * m0;
-      f4 X[NH + 1][4][2];
-      float mu[2], rr[2];
-      unit_forward<NH, KB, JB, NP>(a, sh, ub, Cw, tht + static_cast<size_t>(b) * a.H, m0, nP, t0, X, mu, rr);
-      if (g == 0) {
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const int p = 16 * cb + c;
-          if (p < nP) {
-            const float sg = softplus_f(rr[cb]) + 1e-10f;
-            const int o = t0 + a.s * p + (a.s - 1);
-            ob[a.swap_out ? (o ^ 1) : o] = ub[o + a.k] * sg + mu[cb];
-            if (a.s == 2) {
-              const int oe = t0 + 2 * p;
-              ob[a.swap_out ? (oe ^ 1) : oe] = ub[oe + a.k];
-            }
-            if (o >= a.Lout - a.n_logsig) ls += logf(sg);
-          }
+      f4 X[2][4];
+      float mu, rr;
+      load_unit(a, ub, nullptr, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, nullptr, X[0]);
+      unit_forward<KB, JB, NP>(a, sh, uw, X, mu, rr);
+      if (g == 0 && c < nP) {
+        const float sg = softplus_f(rr) + 1e-10f;
+        const int oq = a.s * c + (a.s - 1);
+        const int o = t0 + oq;
+        ob[a.swap_out ? (o ^ 1) : o] = uw[oq + a.k] * sg + mu;
+        if (a.s == 2) {
+          const int oe = t0 + 2 * c;
+          ob[a.swap_out ? (oe ^ 1) : oe] = uw[2 * c + a.k];
         }
+        if (o >= a.Lout - a.n_logsig) ls += logf(sg);
       }
     }
     const float v = wave_sum(ls);
@@ -420,22 +427,24 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 // backward kernel: one work item per wave; tiles outer, samples inner
 // ---------------------------------------------------------------------------
-template <int NH, int KB, int JB, int NP>
-__global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+template <int KB, int JB, int NP>
+__global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const float* __restrict__ gout, const float* __restrict__ dls,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ du, float* __restrict__ dC_slab,
                                                     float* __restrict__ dth_slab, float* __restrict__ dW_slab,
                                                     float* __restrict__ halo) {
-  static_assert(NH == 1, "flow5 backward: one hidden layer");
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
-  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ Shared<KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][2][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][HP];
   __shared__ float carry[NW][S][KP];
-  __shared__ float gsc[NW][4][P];              // go (= d mu), sigma, go (even, stride 2), d r
+  __shared__ float gsc[NW][3][P];              // sigma, d r, go even (stride 2)
+  __shared__ float uwin[NW][UW];
+  __shared__ float gwin[NW][64];
+  __shared__ float dscr[NW][KP][P];            // dcon [j][p]
   load_shared(sh, img, cst);
   for (int i = threadIdx.x; i < NW * S * HP; i += NT) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW * S * KP; i += NT) (&carry[0][0][0])[i] = 0.f;
@@ -450,10 +459,12 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
   __bf16* xi_l = timg[w][0][NPL - 1];
   __bf16* dz_h = timg[w][1][0];
   __bf16* dz_l = timg[w][1][NPL - 1];
-  float* dsc = reinterpret_cast<float*>(&timg[w][0][0][0]);  // dcon [j][p] fp32, aliases slot 0 (after its reads)
+  float* dsc = &dscr[w][0][0];
   float* mycarry = &carry[w][0][0];
-  const float* whmu = &sh.cst[NH * HP];
-  const float* whr = &sh.cst[NH * HP + HP];
+  float* uw = uwin[w];
+  float* gw = gwin[w];
+  const float* whmu = &sh.cst[HP];
+  const float* whr = &sh.cst[2 * HP];
 
   f4 dW[4][4], dWe[JB][4], dWh[4];
 #pragma unroll
@@ -466,142 +477,121 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
     for (int o = 0; o < 4; ++o) dWe[i][o] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 4; ++i) dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
-  bf8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
+  const bf4 ones4 = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+  const int fwc = 16 + 4 * KB, fis = 18 + 4 * KB + 2 * JB;
 
   for (int m0 = m_lo; m0 < m_hi; m0 += P) {
     const int nP = min(P, m_hi - m0), t0 = a.s * m0, fin = a.s * nP;
-    f4 dCa[4][2];
+    f4 dCa[4];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) dCa[rb][0] = dCa[rb][1] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
     for (int bl = 0; bl < nb; ++bl) {
       fence();
       const int b = b_lo + bl;
       const float* ub = u + static_cast<size_t>(b) * a.L;
-      const int wi = win ? win[b] : 0;
-      const float* Cw = C + static_cast<size_t>(wi) * a.Lh * a.H;
-      f4 X[NH + 1][4][2];
-      float mu[2], rr[2];
-      unit_forward<NH, KB, JB, NP>(a, sh, ub, Cw, tht + static_cast<size_t>(b) * a.H, m0, nP, t0, X, mu, rr);
-      // X0 with its ones row -> transposed image (slot 0) for dW
-      if (a.H < 64 && g == 3) X[0][3][0][3] = X[0][3][1][3] = 1.f;
-      put_image<NP>(xi_h, xi_l, X[0], g, c);
-
-      // ---- head backward ----
       const float* gb = gout + static_cast<size_t>(b) * a.Lout;
+      const int wi = win ? win[b] : 0;
+      const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
       const float dl = dls[b];
-      float gmu[2], gr[2];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int p = 16 * cb + c;
-        const int oq = a.s * p + (a.s - 1);
-        const bool pv = p < nP;
-        const int o = t0 + oq;
-        const float sig = softplus_f(rr[cb]) + 1e-10f;
-        const float gv = pv ? gb[a.swap_out ? (o ^ 1) : o] : 0.f;
-        float dsig = pv ? gv * ub[o + a.k] : 0.f;
-        if (pv && o >= a.Lout - a.n_logsig) dsig += dl / sig;
-        gmu[cb] = gv;
-        gr[cb] = dsig * sigmoid_f(rr[cb]);
-        if (g == 0) {
-          gsc[w][0][p] = gv;
-          gsc[w][1][p] = sig;
-          gsc[w][3][p] = gr[cb];
-          if (a.s == 2) {
-            const int oe = t0 + 2 * p;
-            gsc[w][2][p] = pv ? gb[a.swap_out ? (oe ^ 1) : oe] : 0.f;
-          }
-        }
+      f4 X[2][4];
+      float mu, rr;
+      load_unit(a, ub, gb, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, gw, X[0]);
+      unit_forward<KB, JB, NP>(a, sh, uw, X, mu, rr);
+      // X0 with its ones row -> image (slot 0) for dW; X1 with its ones row -> slot 1 for dW_head
+      if (g == 3) {
+        X[0][3][3] = 1.f;
+        X[1][3][3] = 1.f;
       }
-      // head weight gradient dW_head[h][o] += sum_p X1[h][p] G[o][p] (G = (d mu, d r)); the ones
-      // row of X1 gives the head bias gradient
-      if (a.H < 64 && g == 3) X[1][3][0][3] = X[1][3][1][3] = 1.f;
+      put_image<NP>(xi_h, xi_l, X[0], g, c);
       put_image<NP>(dz_h, dz_l, X[1], g, c);
+
+      // ---- head backward (per position p = c, redundant over g) ----
+      const int oq = a.s * c + (a.s - 1);
+      const bool pv = c < nP;
+      const float sig = softplus_f(rr) + 1e-10f;
+      const float gmu = pv ? gw[oq] : 0.f;
+      float dsig = gmu * uw[oq + a.k];
+      if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl / sig;
+      const float gr = dsig * sigmoid_f(rr);
+      if (g == 0) {
+        gsc[w][0][c] = sig;
+        gsc[w][1][c] = gr;
+        if (a.s == 2) gsc[w][2][c] = pv ? gw[2 * c] : 0.f;
+      }
       fence();
       {
-        float gvv[8];
+        // dW_head[h][o] += sum_p X1[h][p] G[o][p]: B fragment G[p = 4 g + jj][o = c]
+        f4 gv4;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) gvv[jj] = c < 2 ? gsc[w][c == 0 ? 0 : 3][8 * g + jj] : 0.f;
-        const Fr<NP> gf = split8<NP>(gvv);
+        for (int jj = 0; jj < 4; ++jj) {
+          const int p = 4 * g + jj;
+          const float g0 = p < nP ? gw[a.s * p + (a.s - 1)] : 0.f;
+          const float g1 = gsc[w][1][p];
+          gv4[jj] = c == 0 ? g0 : (c == 1 ? g1 : 0.f);
+        }
+        const Fr4<NP> gf = split4<NP>(gv4);
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(dz_h, dz_l, hb, g, c), gf, dWh[hb]);
       }
-      // dX1 = w_mu gmu + w_r gr; dz1 = dX1 * elu'(E1)
-      f4 D[4][2];
+      // dz1 = (w_mu gmu + w_r gr) * elu'(E1)
+      f4 D[4];
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const f4 wm = *reinterpret_cast<const f4*>(&whmu[16 * rb + 4 * g]);
         const f4 wr = *reinterpret_cast<const f4*>(&whr[16 * rb + 4 * g]);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            D[rb][cb][r] = (wm[r] * gmu[cb] + wr[r] * gr[cb]) * elu_grad_from_out(X[1][rb][cb][r]);
+        for (int r = 0; r < 4; ++r) D[rb][r] = (wm[r] * gmu + wr[r] * gr) * elu_d(X[1][rb][r]);
       }
       put_image<NP>(dz_h, dz_l, D, g, c);
       // dX0 = W dz1 (chain)
       fence();
-      f4 dX[4][2];
+      f4 dX[4];
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib) dX[ib][0] = dX[ib][1] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int ib = 0; ib < 4; ++ib) dX[ib] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks) {
+        const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const Fr<NP> df = chain_frag<NP>(D, ks, cb);
-#pragma unroll
-          for (int ib = 0; ib < 4; ++ib) dX[ib][cb] = mm<NP>(wfrag(sh, 8 * NH + ib * 2 + ks, lane), df, dX[ib][cb]);
-        }
-      // dW1 += X0 dz1^T (transposed images)
+        for (int ib = 0; ib < 4; ++ib) dX[ib] = mm<NP>(wfrag(sh, 8 + ib * 2 + ks, lane), df, dX[ib]);
+      }
+      // dW1 += X0 dz1^T
       fence();
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
-        const Fr<NP> xa = tr_frag<NP>(xi_h, xi_l, ib, g, c);
+        const Fr4<NP> xa = tr_frag<NP>(xi_h, xi_l, ib, g, c);
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) dW[ib][ob] = mm<NP>(xa, tr_frag<NP>(dz_h, dz_l, ob, g, c), dW[ib][ob]);
       }
-      // first layer: dA0 = dX0 * elu'(X0), X0 read back from its image (hi + lo; row 63 held 1:
-      // dX0 is 0 there)
+      // dA0 = dX0 * elu'(X0) (X0 from its image; row 63 held 1 where dX0 is 0)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 4; ++rb) {
+        const f4 x0 = get_own<NP>(xi_h, xi_l, rb, g, c);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const f4 x0 = get_own<NP>(xi_h, xi_l, rb, cb, g, c);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = dX[rb][cb][r] * elu_grad_from_out(x0[r]);
-            D[rb][cb][r] = v;
-            dCa[rb][cb][r] += v;
-          }
-        }
-      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]
+        for (int r = 0; r < 4; ++r) D[rb][r] = dX[rb][r] * elu_d(x0[r]);
+      }
+      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]; dC tile += dA0 (identity selection)
       fence();
-      f4 dcn[JB][2];
+      f4 dcn[JB];
 #pragma unroll
-      for (int jb = 0; jb < JB; ++jb) dcn[jb][0] = dcn[jb][1] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int jb = 0; jb < JB; ++jb) dcn[jb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks) {
+        const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const Fr<NP> df = chain_frag<NP>(D, ks, cb);
+        for (int jb = 0; jb < JB; ++jb) dcn[jb] = mm<NP>(wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
 #pragma unroll
-          for (int jb = 0; jb < JB; ++jb)
-            dcn[jb][cb] = mm<NP>(wfrag(sh, 16 * NH + 4 * KB + jb * 2 + ks, lane), df, dcn[jb][cb]);
-        }
-      // dA0 -> slot 1 image; dW_eps and d theta from its transposed fragments
+        for (int o2 = 0; o2 < 2; ++o2) dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
+      }
+      // dA0 -> slot 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(dz_h, dz_l, D, g, c);
       fence();
       f4 dth4[4];
 #pragma unroll
       for (int hb = 0; hb < 4; ++hb) {
-        const Fr<NP> ta = tr_frag<NP>(dz_h, dz_l, hb, g, c);
-        dth4[hb] = mm_bexact<NP>(ta, ones, f4{0.f, 0.f, 0.f, 0.f});
+        const Fr4<NP> ta = tr_frag<NP>(dz_h, dz_l, hb, g, c);
+        dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) {
-          const Fr<NP> uf = ua_frag<NP>(ub, a.L, a.k, t0, a.s, jb, nP, g, c);
-          dWe[jb][hb] = mm<NP>(uf, ta, dWe[jb][hb]);
-        }
+        for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mm<NP>(ua_frag<NP>(uw, a.s, jb, g, c), ta, dWe[jb][hb]);
       }
       if (c == 0) {
 #pragma unroll
@@ -610,65 +600,45 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
           *dp = *dp + dth4[hb];
         }
       }
-      // dcon -> fp32 scratch [j][p] (slot 0: its transposed reads are done)
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dsc[(16 * jb + 4 * g + r) * P + 16 * cb + c] = dcn[jb][cb][r];
+        for (int r = 0; r < 4; ++r) dsc[(16 * jb + 4 * g + r) * P + c] = dcn[jb][r];
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       {
         float* db = du + static_cast<size_t>(b) * a.L;
-        float vq[2];
-        int qq[2];
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          const int q = lane + 64 * it;
-          qq[it] = q;
+        for (int base = 0; base < fin + a.k; base += 64) {
+          const int q = base + lane;
           float v = 0.f;
-          if (q < fin + a.k) {
-            for (int j = 0; j < a.k; ++j) {
-              const int t = q - j;
-              if (t >= 0) {
-                if (a.s == 1) {
-                  if (t < nP) v += dsc[j * P + t];
-                } else if (!(t & 1) && (t >> 1) < nP) {
-                  v += dsc[j * P + (t >> 1)];
-                }
-              }
-            }
-            const int oq = q - a.k;
-            if (oq >= 0 && oq < fin) {
-              if (a.s == 1) v += gsc[w][0][oq] * gsc[w][1][oq];
-              else v += (oq & 1) ? gsc[w][0][oq >> 1] * gsc[w][1][oq >> 1] : gsc[w][2][oq >> 1];
-            }
-            if (q < a.k) v += mycarry[bl * KP + q];
+          for (int j = 0; j < a.k; ++j) {
+            const int t = q - j;
+            const int pp = a.s == 1 ? t : (t >> 1);
+            const bool ok = t >= 0 && pp < nP && (a.s == 1 || !(t & 1));
+            const float x = dsc[j * P + (pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp))];
+            v += ok ? x : 0.f;
           }
-          vq[it] = v;
-        }
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          const int q = qq[it];
-          if (q < fin) db[t0 + q] = vq[it];
-          else if (q < fin + a.k) mycarry[bl * KP + q - fin] = vq[it];
+          const int oq2 = q - a.k;
+          if (oq2 >= 0 && oq2 < fin) {
+            if (a.s == 1) v += gw[oq2] * gsc[w][0][oq2];
+            else v += (oq2 & 1) ? gw[oq2] * gsc[w][0][oq2 >> 1] : gsc[w][2][oq2 >> 1];
+          }
+          const float cin = mycarry[bl * KP + (q < a.k ? q : 0)];
+          if (q < a.k) v += cin;
+          if (q < fin) db[t0 + q] = v;
+          else if (q < fin + a.k) mycarry[bl * KP + q - fin] = v;
         }
       }
     }
     // tile done: its dC over the group
-    float* dcs = dC_slab + (static_cast<size_t>(grp) * a.Lh + m0) * a.H;
+    if (c < nP) {
+      float* dcs = dC_slab + (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int p = 16 * cb + c;
-      if (p < nP) {
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int h = 16 * rb + 4 * g + r;
-            if (h < a.H) dcs[static_cast<size_t>(p) * a.H + h] = dCa[rb][cb][r];
-          }
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * rb + 4 * g + r;
+          if (h < a.H) dcs[h] = dCa[rb][r];
+        }
     }
   }
 
@@ -685,7 +655,7 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
 
   // ---- weight-gradient partials of this work item (layout of flow4's n_wgrad) ----
   const int H = a.H;
-  const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
+  const int nW = a.k * H + H * H + 3 * H + 2 * H + 2;
   float* ws = dW_slab + static_cast<size_t>(item) * nW;
 #pragma unroll
   for (int jb = 0; jb < JB; ++jb)
@@ -696,7 +666,7 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
         const int j = 16 * jb + 4 * g + r, h = 16 * hb + c;
         if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r];
       }
-  const int off_w = a.k * H, off_b = off_w + NH * H * H;
+  const int off_w = a.k * H, off_b = off_w + H * H;
 #pragma unroll
   for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
@@ -709,9 +679,8 @@ __global__ __launch_bounds__(NT, 1) void bwd_kernel(KArgs a, const float* __rest
           else if (hi == 63) ws[off_b + ho] = dW[ib][ob][r];  // the ones row: bias gradient
         }
       }
-  // bn gamma / beta partials: zero (no BN on this path)
-  for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;
-  const int off_h = off_b + 3 * NH * H;
+  for (int i = lane; i < 2 * H; i += 64) ws[off_b + H + i] = 0.f;  // bn gamma / beta: no BN here
+  const int off_h = off_b + 3 * H;
   if (c < 2) {
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb)
@@ -766,6 +735,7 @@ static int np_of(const VissmFlowDesc* d) { return d->precision == VISSM_PREC_BF1
 struct Ws {
   bf8* img;
   float* cst;
+  float *Cp, *thp;
   float* ls_slab;                                        // fwd
   float *dC_slab, *dth_slab, *dW_slab, *halo, *wred;     // bwd
 };
@@ -776,8 +746,10 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   Ws t{};
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
   const int NPL = np_of(d) == 3 ? 2 : 1;
-  t.img = reinterpret_cast<bf8*>(take(static_cast<size_t>(n_frags(d->n_hidden, KB, JB)) * NPL * 64 * sizeof(bf8)));
-  t.cst = reinterpret_cast<float*>(take(((d->n_hidden + 2) * HP + 4) * sizeof(float)));
+  t.img = reinterpret_cast<bf8*>(take(static_cast<size_t>(n_frags(KB, JB)) * NPL * 64 * sizeof(bf8)));
+  t.cst = reinterpret_cast<float*>(take((3 * HP + 4) * sizeof(float)));
+  t.Cp = reinterpret_cast<float*>(take(static_cast<size_t>(d->n_win) * g.Lh * HP * 4));
+  t.thp = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * HP * 4));
   if (!backward) {
     t.ls_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * 4));
   } else {
@@ -860,23 +832,32 @@ size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
   do {                                                                                             \
     if (NP == 3) {                                                                                 \
       switch (JB) {                                                                                \
-        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 3>), __VA_ARGS__); break;                       \
-        default: hipLaunchKernelGGL((KERNEL<1, 1, 2, 3>), __VA_ARGS__); break;                      \
+        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 3>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<1, 2, 3>), __VA_ARGS__); break;                      \
       }                                                                                            \
     } else {                                                                                       \
       switch (JB) {                                                                                \
-        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 1>), __VA_ARGS__); break;                       \
-        case 2: hipLaunchKernelGGL((KERNEL<1, 1, 2, 1>), __VA_ARGS__); break;                       \
-        case 3: hipLaunchKernelGGL((KERNEL<1, 2, 3, 1>), __VA_ARGS__); break;                       \
-        default: hipLaunchKernelGGL((KERNEL<1, 2, 4, 1>), __VA_ARGS__); break;                      \
+        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1>), __VA_ARGS__); break;                       \
+        case 2: hipLaunchKernelGGL((KERNEL<1, 2, 1>), __VA_ARGS__); break;                       \
+        case 3: hipLaunchKernelGGL((KERNEL<2, 3, 1>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<2, 4, 1>), __VA_ARGS__); break;                      \
       }                                                                                            \
     }                                                                                              \
   } while (0)
 
+static void launch_pad(const VissmFlowDesc* d, const Geom& g, const float* C, const float* tht, const Ws& ws,
+                       hipStream_t st) {
+  const int64_t nC = static_cast<int64_t>(d->n_win) * g.Lh, nT = d->B;
+  hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nC * HP + 255) / 256)), dim3(256), 0, st, C, ws.Cp, nC,
+                     d->H);
+  hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nT * HP + 255) / 256)), dim3(256), 0, st, tht, ws.thp, nT,
+                     d->H);
+}
+
 static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, hipStream_t st) {
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
-  hipLaunchKernelGGL(prep_kernel, dim3(n_frags(d->n_hidden, KB, JB)), dim3(64), 0, st, *w, d->H, d->k, d->n_hidden,
-                     np_of(d), KB, JB, ws.img, ws.cst);
+  hipLaunchKernelGGL(prep_kernel, dim3(n_frags(KB, JB)), dim3(64), 0, st, *w, d->H, d->k, np_of(d), KB, JB, ws.img,
+                     ws.cst);
 }
 
 int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -887,12 +868,13 @@ int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   Ws ws;
   ws_layout(d, g, false, reinterpret_cast<char*>(workspace), &ws);
   launch_prep(d, w, ws, st);
+  launch_pad(d, g, C, theta_term, ws, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  FLOW5_DISPATCH(fwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, C, wn, theta_term, ws.img, ws.cst,
+  FLOW5_DISPATCH(fwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst,
                  u_next, ws.ls_slab);
   VISSM_CHECK_LAUNCH("flow5_fwd");
   prof_end(VISSM_PROF_FLOW_FWD, st);
@@ -907,12 +889,13 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws);
   launch_prep(d, w, ws, st);
+  launch_pad(d, g, C, theta_term, ws, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
-  FLOW5_DISPATCH(bwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, C, wn, theta_term, du_next, dlogsig,
+  FLOW5_DISPATCH(bwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next, dlogsig,
                  ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
