@@ -140,7 +140,9 @@ __host__ __device__ __forceinline__ int hperm(int ks, int g, int j) {
 }
 
 __device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
-__device__ __forceinline__ float elu_d(float y) { return y < 0.f ? y + 1.f : 1.f; }
+__device__ __forceinline__ float elu_d(float y) { return fminf(y, 0.f) + 1.f; }
+__device__ __forceinline__ float softplus_fast(float x) { return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x))); }
+__device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------
 // weight fragments (8 bf16 per lane): [frag][plane (hi, lo)][lane]
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
       load_unit(a, ub, nullptr, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, nullptr, X[0]);
       unit_forward<KB, JB, NP>(a, sh, uw, X, mu, rr);
       if (g == 0 && c < nP) {
-        const float sg = softplus_f(rr) + 1e-10f;
+        const float sg = softplus_fast(rr) + 1e-10f;
         const int oq = a.s * c + (a.s - 1);
         const int o = t0 + oq;
         ob[a.swap_out ? (o ^ 1) : o] = uw[oq + a.k] * sg + mu;
@@ -508,11 +510,11 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // ---- head backward (per position p = c, redundant over g) ----
       const int oq = a.s * c + (a.s - 1);
       const bool pv = c < nP;
-      const float sig = softplus_f(rr) + 1e-10f;
+      const float sig = softplus_fast(rr) + 1e-10f;
       const float gmu = pv ? gw[oq] : 0.f;
       float dsig = gmu * uw[oq + a.k];
       if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl / sig;
-      const float gr = dsig * sigmoid_f(rr);
+      const float gr = dsig * sigmoid_fast(rr);
       if (g == 0) {
         gsc[w][0][c] = sig;
         gsc[w][1][c] = gr;
@@ -610,6 +612,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         for (int base = 0; base < fin + a.k; base += 64) {
           const int q = base + lane;
           float v = 0.f;
+#pragma unroll 4
           for (int j = 0; j < a.k; ++j) {
             const int t = q - j;
             const int pp = a.s == 1 ? t : (t >> 1);
