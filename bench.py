@@ -29,13 +29,31 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "latent-state transitions/sec (batch_dims×T per step), AR(1) T=5000, 1/2/4/8 GPU"
-PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0}  # MI355X dense (MI355X_MICROARCH.md)
+PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3}  # MI355X dense (MI355X_MICROARCH.md);
+# bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak
 
 
 def flow_bwd_flops_per_position(k, H, nh):
     """Algorithmic FLOPs of the flow backward per (sample, head position): recompute forward
     (2kH + 2 nh H^2 + 4H) + hidden dX and dW (4 nh H^2) + head (8H) + first-layer dW_eps and dU (4kH)."""
     return 6 * k * H + 6 * nh * H * H + 12 * H
+
+
+def measured_traffic(args):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (profiles/traffic.json, written by scripts/traffic_from_pmc.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes of this same command), or None when no summary matches."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get(args.precision)
+        if e and e.get("B") == args.B and e.get("T") == args.T and e.get("k") == args.k:
+            return e["bytes_per_launch"]
+    except (ValueError, KeyError):
+        pass
+    return None
 
 
 def cpu_baseline(args, obs, ob, tt):
@@ -78,7 +96,9 @@ def main():
     ap.add_argument("--B", type=int, default=65536, help="trajectories per GPU")
     ap.add_argument("--T", type=int, default=5000)
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="bf16",
+                    help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
+                         "reductions and the optimizer are fp32 throughout")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-B", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
@@ -153,6 +173,8 @@ def main():
     avg_launch_s = bwd_ms / max(bwd_n, 1) / 1e3
     achieved = flops_per_launch / avg_launch_s / 1e12 if bwd_n else None
     peak = PEAKS_TFLOPS[args.precision]
+    kernel = "flow5::bwd_kernel (bf16 matrix cores)" if args.precision != "fp32" else "flow4::bwd_kernel (fp32 matrix cores)"
+    traffic = measured_traffic(args)
     value = world * B * T * args.steps / elapsed
     res = {
         "metric": METRIC,
@@ -173,8 +195,8 @@ def main():
                                f"(BASELINE batch_dims -> B)", "global_batch": B * world, "seq_len": T,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": (achieved / peak) if achieved else None, "traffic": None,
-                     "kernel": "flow_bwd_kernel", "flops_per_launch": flops_per_launch,
+                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                     "kernel": kernel, "flops_per_launch": flops_per_launch,
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }

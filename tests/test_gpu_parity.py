@@ -62,6 +62,35 @@ def test_family_parity_multi_window(family, k, T, starts):
     _check(run_parity_case(family, len(starts), 40, k, 2, 24, 5, 3, device=DEV, T=T, starts=starts))
 
 
+# Matrix-core bf16 paths (flow_v5) against the same float64 oracle.  bf16x3 (split operands,
+# ~2^-16 relative per product) keeps the north-star ELBO bar of 1e-4; plain bf16 operands
+# (the BASELINE config's precision) are held to 3e-3 on the ELBO and 5e-2 on the gradient.
+BF16X3_TOL = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
+BF16_TOL = dict(elbo_tol=3e-3, grad_tol=5e-2, param_tol=2e-1)
+
+
+@pytest.mark.parametrize("prec,tol", [(2, BF16X3_TOL), (1, BF16_TOL)])
+@pytest.mark.parametrize("B,M,k,nf,H,nl,fw", [
+    (4, 24, 4, 2, 16, 3, 3),
+    (40, 30, 8, 3, 50, 3, 10),    # AR-cfg flow shape (k = 8, H = 50, one hidden layer)
+    (2, 5, 1, 1, 8, 3, 2),
+])
+def test_ar_parity_matrix_core(prec, tol, B, M, k, nf, H, nl, fw):
+    _check(run_parity_case("ar", B, M, k, nf, H, nl, fw, device=DEV, precision=prec), **tol)
+
+
+def test_ar_parity_matrix_core_paper_and_multiwindow():
+    _check(run_parity_case("ar", 3, 50, 50, 3, 50, 3, 10, device=DEV, precision=1), **BF16_TOL)  # k = 50 (bf16 only)
+    starts = [0, 50, 100, 100, 250, 0]
+    _check(run_parity_case("ar", 6, 50, 10, 3, 32, 3, 10, device=DEV, T=300, starts=starts, precision=2), **BF16X3_TOL)
+
+
+def test_matrix_core_deterministic():
+    a = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV, precision=1)
+    b = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV, precision=1)
+    assert a["per_param"] == b["per_param"] and a["elbo_rel_err"] == b["elbo_rel_err"]
+
+
 def test_ar_deterministic():
     a = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV)
     b = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV)
