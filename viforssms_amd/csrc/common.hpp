@@ -106,6 +106,8 @@ constexpr float kLog2Pi = 1.8378770664093453f;
 constexpr float kBnScale = 0.99950037468777f;  // 1/sqrt(1 + 1e-3)
 
 int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipStream_t st);
+// same result, two passes for few columns / many rows; uses the slab's part-head rows as scratch
+int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hipStream_t st);
 
 // opt-in event timing of main kernels (vissm_profile_*)
 bool prof_on();

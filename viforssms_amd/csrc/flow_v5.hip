@@ -910,7 +910,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   int rc;
   if (d->n_win == 1) {
-    rc = launch_reduce_rows(ws.dC_slab, dC, g.n_groups, nC, st);
+    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_groups, nC, st);
     if (rc) return rc;
   } else {
     dim3 rg(static_cast<unsigned>((nC + 255) / 256), d->n_win);
@@ -921,7 +921,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   rc = launch_reduce_rows(ws.dth_slab, dtheta_term, g.n_chunks, static_cast<int64_t>(d->B) * d->H, st);
   if (rc) return rc;
   const int nW = n_wgrad(d);
-  rc = launch_reduce_rows(ws.dW_slab, ws.wred, g.n_items, nW, st);
+  rc = launch_reduce_rows_inplace(ws.dW_slab, ws.wred, g.n_items, nW, st);
   if (rc) return rc;
   hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *gr, d->k,
                      d->H, d->n_hidden);

@@ -66,23 +66,64 @@ __global__ __launch_bounds__(256) void base_logprob_kernel(const float* __restri
 // out[c] = sum_r slab[r][c], fixed order.  Columns across threads (coalesced),
 // rows split in chunks of RCH across blockIdx.y then summed in order by a second pass.
 // ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_rows_strided_kernel(const float* __restrict__ slab,
+                                                                  float* __restrict__ out, int64_t R, int64_t N,
+                                                                  int64_t row_stride) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int64_t r = 0; r < R; ++r) s += slab[r * row_stride + c];
+  out[c] = s;
+}
+
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                          int64_t R, int64_t N, int64_t rows_per_part) {
+                                                          int64_t R, int64_t N, int64_t rows_per_part,
+                                                          int64_t out_stride) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (c >= N) return;
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
   const int64_t r1 = min(R, r0 + rows_per_part);
+  // fixed order: r0, r0+1, ... (four loads in flight, summed in row order)
   float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += slab[r * N + c];
-  out[static_cast<int64_t>(blockIdx.y) * N + c] = s;
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    const float a0 = slab[r * N + c], a1 = slab[(r + 1) * N + c], a2 = slab[(r + 2) * N + c],
+                a3 = slab[(r + 3) * N + c];
+    s += a0;
+    s += a1;
+    s += a2;
+    s += a3;
+  }
+  for (; r < r1; ++r) s += slab[r * N + c];
+  out[static_cast<int64_t>(blockIdx.y) * out_stride + c] = s;
 }
 
 int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipStream_t st) {
   if (R <= 0 || N <= 0) return VISSM_OK;
   // single pass: rows summed sequentially per column (deterministic)
   dim3 grid(static_cast<unsigned>((N + 255) / 256), 1);
-  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(256), 0, st, slab, out, R, N, R);
+  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(256), 0, st, slab, out, R, N, R, N);
   VISSM_CHECK_LAUNCH("reduce_rows");
+  return VISSM_OK;
+}
+
+int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hipStream_t st) {
+  if (R <= 0 || N <= 0) return VISSM_OK;
+  // two deterministic passes when there are few columns: parts of rpp rows each are summed in
+  // order into the part's first row (in place: no other part reads it), then the parts in order
+  const int64_t want_threads = 1 << 17;
+  int64_t parts = (want_threads + N - 1) / N;
+  parts = std::min<int64_t>(parts, R / 8);
+  if (parts <= 1) return launch_reduce_rows(slab, out, R, N, st);
+  const int64_t rpp = (R + parts - 1) / parts;
+  parts = (R + rpp - 1) / rpp;
+  dim3 g1(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(parts));
+  hipLaunchKernelGGL(reduce_rows_kernel, g1, dim3(256), 0, st, slab, slab, R, N, rpp, rpp * N);
+  VISSM_CHECK_LAUNCH("reduce_rows_p1");
+  // pass 2 over the part heads: rows 0, rpp, 2 rpp, ... == a slab of `parts` rows with stride rpp*N
+  dim3 g2(static_cast<unsigned>((N + 255) / 256), 1);
+  hipLaunchKernelGGL(reduce_rows_strided_kernel, g2, dim3(256), 0, st, slab, out, parts, N, rpp * N);
+  VISSM_CHECK_LAUNCH("reduce_rows_p2");
   return VISSM_OK;
 }
 
