@@ -40,7 +40,8 @@ constexpr int HP = 64;
 constexpr int S = 16;
 constexpr int NW = 4;
 constexpr int NT = 64 * NW;
-constexpr int UW = 128;  // u window staged per unit: s * P + k <= 96
+constexpr int UW = 128;
+constexpr int DTH = 56;  // d theta rows kept per sample (H <= DTH): keeps the backward block <= 80 KB of LDS  // u window staged per unit: s * P + k <= 96
 
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
@@ -140,7 +141,7 @@ __host__ __device__ __forceinline__ int hperm(int ks, int g, int j) {
 }
 
 __device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
-__device__ __forceinline__ float elu_d(float y) { return fminf(y, 0.f) + 1.f; }
+__device__ __forceinline__ float elu_d(float y) { return __builtin_amdgcn_fmed3f(y, -2.f, 0.f) + 1.f; }  // y >= -1
 __device__ __forceinline__ float softplus_fast(float x) { return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x))); }
 __device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + __expf(-x)); }
 
@@ -441,15 +442,22 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
   __shared__ Shared<KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][2][NPL][P * HP];  // [wave][slot][plane][p][h]
-  __shared__ float dthl[NW][S][HP];
+  __shared__ float dthl[NW][S][DTH];
   __shared__ float carry[NW][S][KP];
   __shared__ float gsc[NW][3][P];              // sigma, d r, go even (stride 2)
   __shared__ float uwin[NW][UW];
   __shared__ float gwin[NW][64];
-  __shared__ float dscr[NW][KP][P];            // dcon [j][p]
+  // dcon[j][p] stored at its output position q = s p + j of row j (other columns stay zero),
+  // so du[q] = sum_{j<k} row_j[q] needs no masks
+  // (k > 32: the unpadded [j][p] layout with a masked sum keeps the block's LDS in bounds)
+  constexpr bool PADDED = JB <= 2;
+  constexpr int QW = PADDED ? 2 * P + KP : P;
+  __shared__ float dscr[NW][KP][QW];
   load_shared(sh, img, cst);
-  for (int i = threadIdx.x; i < NW * S * HP; i += NT) (&dthl[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW * S * DTH; i += NT) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW * S * KP; i += NT) (&carry[0][0][0])[i] = 0.f;
+  if constexpr (PADDED)
+    for (int i = threadIdx.x; i < NW * KP * QW; i += NT) (&dscr[0][0][0])[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int item = blockIdx.x * NW + w;
@@ -598,27 +606,38 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       if (c == 0) {
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
-          f4* dp = reinterpret_cast<f4*>(&dthl[w][bl][16 * hb + 4 * g]);
-          *dp = *dp + dth4[hb];
+          if (16 * hb + 4 * g < DTH) {
+            f4* dp = reinterpret_cast<f4*>(&dthl[w][bl][16 * hb + 4 * g]);
+            *dp = *dp + dth4[hb];
+          }
         }
       }
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dsc[(16 * jb + 4 * g + r) * P + c] = dcn[jb][r];
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * jb + 4 * g + r;
+          dsc[j * QW + (PADDED ? a.s * c + j : c)] = dcn[jb][r];
+        }
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       {
         float* db = du + static_cast<size_t>(b) * a.L;
         for (int base = 0; base < fin + a.k; base += 64) {
           const int q = base + lane;
           float v = 0.f;
+          if constexpr (PADDED) {
+            const int qc = q < QW ? q : QW - 1;
 #pragma unroll 4
-          for (int j = 0; j < a.k; ++j) {
-            const int t = q - j;
-            const int pp = a.s == 1 ? t : (t >> 1);
-            const bool ok = t >= 0 && pp < nP && (a.s == 1 || !(t & 1));
-            const float x = dsc[j * P + (pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp))];
-            v += ok ? x : 0.f;
+            for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
+          } else {
+#pragma unroll 4
+            for (int j = 0; j < a.k; ++j) {
+              const int t = q - j;
+              const int pp = a.s == 1 ? t : (t >> 1);
+              const bool ok = t >= 0 && pp < nP && (a.s == 1 || !(t & 1));
+              const float x = dsc[j * P + (pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp))];
+              v += ok ? x : 0.f;
+            }
           }
           const int oq2 = q - a.k;
           if (oq2 >= 0 && oq2 < fin) {
@@ -823,7 +842,7 @@ using namespace flow5;
 bool flow5_supports(const VissmFlowDesc* d) {
   // bf16x3 keeps hi and lo images in LDS: k <= 32 there (k <= 64 for bf16)
   return (d->precision == VISSM_PREC_BF16 || (d->precision == VISSM_PREC_BF16X3 && d->k <= 32)) &&
-         d->n_hidden == 1 && !d->bn && d->H <= 63 && d->k <= 64;
+         d->n_hidden == 1 && !d->bn && d->H <= DTH && d->k <= 64;
 }
 
 size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
