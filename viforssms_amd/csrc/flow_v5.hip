@@ -32,6 +32,8 @@
 // other shapes run on flow_v4 (exact fp32).
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace vissm {
 namespace flow5 {
 
@@ -158,6 +160,7 @@ __host__ __device__ constexpr int n_frags(int KB, int JB) { return 16 + 4 * KB +
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
+  int abl;  // phase-ablation mask for timing experiments (VISSM_V5_ABLATE; 0 in production)
 };
 
 __global__ void prep_kernel(VissmFlowParams w, int H, int k, int NP, int KB, int JB, bf8* __restrict__ img,
@@ -540,8 +543,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           gv4[jj] = c == 0 ? g0 : (c == 1 ? g1 : 0.f);
         }
         const Fr4<NP> gf = split4<NP>(gv4);
+        if (!(a.abl & 1))
 #pragma unroll
-        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(dz_h, dz_l, hb, g, c), gf, dWh[hb]);
+          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(dz_h, dz_l, hb, g, c), gf, dWh[hb]);
       }
       // dz1 = (w_mu gmu + w_r gr) * elu'(E1)
       f4 D[4];
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // dW1 += X0 dz1^T
       fence();
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib) {
+      for (int ib = 0; ib < 4 * !(a.abl & 2); ++ib) {
         const Fr4<NP> xa = tr_frag<NP>(xi_h, xi_l, ib, g, c);
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) dW[ib][ob] = mm<NP>(xa, tr_frag<NP>(dz_h, dz_l, ob, g, c), dW[ib][ob]);
@@ -590,14 +594,15 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dcn[jb] = mm<NP>(wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
 #pragma unroll
-        for (int o2 = 0; o2 < 2; ++o2) dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
+        for (int o2 = 0; o2 < 2 * !(a.abl & 16); ++o2)
+          dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
       }
       // dA0 -> slot 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(dz_h, dz_l, D, g, c);
       fence();
-      f4 dth4[4];
+      f4 dth4[4] = {};
 #pragma unroll
-      for (int hb = 0; hb < 4; ++hb) {
+      for (int hb = 0; hb < 4 * !(a.abl & 4); ++hb) {
         const Fr4<NP> ta = tr_frag<NP>(dz_h, dz_l, hb, g, c);
         dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -622,7 +627,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       {
         float* db = du + static_cast<size_t>(b) * a.L;
-        for (int base = 0; base < fin + a.k; base += 64) {
+        for (int base = 0; base < (a.abl & 8 ? 0 : fin + a.k); base += 64) {
           const int q = base + lane;
           float v = 0.f;
           if constexpr (PADDED) {
@@ -790,6 +795,8 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
+  const char* ab = std::getenv("VISSM_V5_ABLATE");
+  a.abl = ab ? std::atoi(ab) : 0;
   return a;
 }
 
