@@ -11,7 +11,8 @@ import os
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvissm.so")
+# VISSM_LIB selects an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("VISSM_LIB", os.path.join(_HERE, "libvissm.so"))
 
 VISSM_PREC_FP32 = 0
 VISSM_PREC_BF16 = 1
