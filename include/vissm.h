@@ -105,7 +105,8 @@ typedef struct {        /* outputs of the backward: written, not accumulated */
   float* w_head; float* b_head;
 } VissmFlowGrads;
 
-/* Selects the flow implementation for A/B measurements (4 = matrix cores,
+/* Selects the fp32 flow implementation for A/B measurements (default 0 = by shape:
+ * 4 for one hidden layer, 2 otherwise; 4 = matrix cores,
  * latency-hiding [default]; 3 = matrix cores, 8-wave blocks; 2 = matrix cores,
  * 4-wave blocks; 1 = VALU/LDS).
  * 0 only queries.  Returns the previous selection. */

@@ -39,12 +39,20 @@ int flow5_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 
 static int g_impl = 0;  // 0 = not chosen yet
 
-static int impl() {
+static int impl_choice() {
   if (g_impl == 0) {
     const char* e = std::getenv("VISSM_FLOW_IMPL");
-    g_impl = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
+    g_impl = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : -1;  // -1: by shape
   }
   return g_impl;
+}
+
+// fp32 path: flow4 for the one-hidden-layer (AR) shapes; flow2 for deeper heads, where flow4's
+// register-resident weights do not apply and it measured slower (LV-like shape: 64 vs 76 ms bwd)
+static int impl_for(const VissmFlowDesc* d) {
+  const int c = impl_choice();
+  if (c > 0) return c;
+  return d->n_hidden <= 1 ? 4 : 2;
 }
 
 static int validate(const VissmFlowDesc* d) {
@@ -76,15 +84,15 @@ extern "C" {
 
 int vissm_flow_set_impl(int32_t which) {
   VISSM_CHECK_ARG(which >= 0 && which <= 4, "flow_set_impl: %d not in [0,4]", which);
-  const int prev = impl();
+  const int prev = impl_choice();
   if (which > 0) vissm::g_impl = which;
-  return prev;
+  return prev < 0 ? 0 : prev;
 }
 
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
   if (use_v5(d)) return flow5_workspace_size(d, backward);
-  switch (impl()) {
+  switch (impl_for(d)) {
     case 1: return flow1_workspace_size(d, backward);
     case 2: return flow2_workspace_size(d, backward);
     case 3: return flow3_workspace_size(d, backward);
@@ -104,7 +112,7 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
   if (use_v5(d)) return flow5_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-  switch (impl()) {
+  switch (impl_for(d)) {
     case 1: return flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
     case 2: return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
     case 3: return flow3_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
@@ -128,7 +136,7 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
     return flow5_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
-  switch (impl()) {
+  switch (impl_for(d)) {
     case 1: return flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
                              ws_bytes, st);
     case 2: return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
