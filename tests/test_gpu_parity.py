@@ -85,6 +85,26 @@ def test_ar_parity_matrix_core_paper_and_multiwindow():
     _check(run_parity_case("ar", 6, 50, 10, 3, 32, 3, 10, device=DEV, T=300, starts=starts, precision=2), **BF16X3_TOL)
 
 
+# LV / SV / FHN heads (3 hidden layers, BN folded into the next layer) on the bf16 kernels
+BF16_FAMILY_TOL = dict(elbo_tol=5e-3, grad_tol=2e-2, param_tol=2e-1)
+
+
+@pytest.mark.parametrize("family,B,M,k,nf,H,nl,fw", [
+    ("lv", 4, 24, 4, 2, 16, 5, 3),
+    ("lv", 3, 50, 20, 3, 50, 5, 10),
+    ("sv", 4, 24, 6, 2, 16, 5, 3),
+    ("sv", 3, 52, 50, 5, 50, 5, 5),
+    ("fhn", 3, 50, 20, 3, 50, 5, 10),
+])
+def test_family_parity_matrix_core(family, B, M, k, nf, H, nl, fw):
+    _check(run_parity_case(family, B, M, k, nf, H, nl, fw, device=DEV, precision=1), **BF16_FAMILY_TOL)
+
+
+def test_family_parity_matrix_core_multi_window():
+    _check(run_parity_case("fhn", 5, 40, 6, 2, 24, 5, 3, device=DEV, T=160, starts=[120, 0, 40, 40, 80], precision=1),
+           **BF16_FAMILY_TOL)
+
+
 def test_matrix_core_deterministic():
     a = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV, precision=1)
     b = run_parity_case("ar", 8, 40, 6, 2, 24, 3, 4, device=DEV, precision=1)

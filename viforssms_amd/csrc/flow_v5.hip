@@ -151,37 +151,51 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + 
 
 // ---------------------------------------------------------------------------
 // weight fragments (8 bf16 per lane): [frag][plane (hi, lo)][lane]
-//   WF(ob, ks)   ob*2 + ks          forward hidden    A[h_out][h_in perm]
-//   WB(ib, ks)   8 + ib*2 + ks      dX = W dZ         A[h_in][h_out perm]
-//   WE(kb, ob)   16 + kb*4 + ob     layer 0           A[h][j]
-//   WC(jb, ks)   16 + 4KB + jb*2+ks dcon              A[j][h perm]
-//   WH(ks)       16 + 4KB + 2JB+ks  head              A[o][h perm]
-//   IS(ob)       18 + 4KB + 2JB+ob  dC selection      A[h][h perm] = identity (exact; hi plane only)
+//   WF(l, ob, ks)  l*8 + ob*2 + ks          forward hidden l   A[h_out][h_in perm]
+//   WB(l, ib, ks)  8NH + l*8 + ib*2 + ks    dI = W dZ          A[h_in][h_out perm]
+//   WE(kb, ob)     16NH + kb*4 + ob         layer 0            A[h][j]
+//   WC(jb, ks)     16NH + 4KB + jb*2 + ks   dcon               A[j][h perm]
+//   WH(ks)         16NH + 4KB + 2JB + ks    head               A[o][h perm]
+//   IS(ob)         16NH + 4KB + 2JB + 2+ob  dC selection       identity (exact; hi plane only)
+// With batch_normalization(training=False) after each hidden ELU (LV / SV / FHN), the BN affine
+// x = gamma' e + beta is folded into the layer that consumes it: W~ = diag(gamma') W and
+// b~ = b + W^T beta (head likewise), so the kernels only see ELU outputs E; the BN and
+// unfolded weight gradients are recovered from the reduced sums in scatter_wgrad_kernel.
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int n_frags(int KB, int JB) { return 16 + 4 * KB + 2 * JB + 2 + 4; }
+__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * NH + 4 * KB + 2 * JB + 6; }
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
   int abl;  // phase-ablation mask for timing experiments (VISSM_V5_ABLATE; 0 in production)
 };
 
-__global__ void prep_kernel(VissmFlowParams w, int H, int k, int NP, int KB, int JB, bf8* __restrict__ img,
-                            float* __restrict__ cst) {
+// folded hidden weight W~_l[hin][hout] and head weight W~_h[h][o]
+__device__ __forceinline__ float wt_hid(const VissmFlowParams& w, int H, int bn, int l, int hin, int hout) {
+  const float x = w.w_hid[(static_cast<size_t>(l) * H + hin) * H + hout];
+  return (bn && l > 0) ? x * w.bn_g[(l - 1) * H + hin] * kBnScale : x;
+}
+__device__ __forceinline__ float wt_head(const VissmFlowParams& w, int H, int bn, int nh, int h, int o) {
+  const float x = w.w_head[h * 2 + o];
+  return (bn && nh > 0) ? x * w.bn_g[(nh - 1) * H + h] * kBnScale : x;
+}
+
+__global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int NP, int KB, int JB,
+                            bf8* __restrict__ img, float* __restrict__ cst) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   const int NPL = NP == 3 ? 2 : 1;
   float v[8];
   for (int j = 0; j < 8; ++j) {
     float x = 0.f;
     int r = f;
-    if (r < 8) {  // WF
-      const int ob = r >> 1, ks = r & 1;
+    if (r < 8 * nh) {  // WF
+      const int l = r >> 3, ob = (r >> 1) & 3, ks = r & 1;
       const int hin = hperm(ks, g, j), hout = 16 * ob + c;
-      if (hin < H && hout < H) x = w.w_hid[hin * H + hout];
-    } else if ((r -= 8) < 8) {  // WB
-      const int ib = r >> 1, ks = r & 1;
+      if (hin < H && hout < H) x = wt_hid(w, H, bn, l, hin, hout);
+    } else if ((r -= 8 * nh) < 8 * nh) {  // WB
+      const int l = r >> 3, ib = (r >> 1) & 3, ks = r & 1;
       const int hin = 16 * ib + c, hout = hperm(ks, g, j);
-      if (hin < H && hout < H) x = w.w_hid[hin * H + hout];
-    } else if ((r -= 8) < 4 * KB) {  // WE
+      if (hin < H && hout < H) x = wt_hid(w, H, bn, l, hin, hout);
+    } else if ((r -= 8 * nh) < 4 * KB) {  // WE
       const int kb = r >> 2, ob = r & 3;
       const int jt = 32 * kb + 8 * g + j, h = 16 * ob + c;
       if (jt < k && h < H) x = w.w_eps[jt * H + h];
@@ -191,7 +205,7 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int NP, int KB, int
       if (jt < k && h < H) x = w.w_eps[jt * H + h];
     } else if ((r -= 2 * JB) < 2) {  // WH
       const int h = hperm(r, g, j);
-      if (c < 2 && h < H) x = w.w_head[h * 2 + c];
+      if (c < 2 && h < H) x = wt_head(w, H, bn, nh, h, c);
     } else {  // IS
       const int ob = r - 2;
       x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
@@ -206,11 +220,25 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int NP, int KB, int
   img[(f * NPL + 0) * 64 + lane] = hi;
   if (NPL == 2) img[(f * NPL + 1) * 64 + lane] = lo;
   if (f == 0) {
-    // constants: bias[64], w_head[2][64], b_head[2]
-    cst[lane] = lane < H ? w.b_hid[lane] : 0.f;
-    cst[HP + lane] = lane < H ? w.w_head[lane * 2 + 0] : 0.f;
-    cst[2 * HP + lane] = lane < H ? w.w_head[lane * 2 + 1] : 0.f;
-    if (lane < 2) cst[3 * HP + lane] = w.b_head[lane];
+    // constants: folded biases [nh][64], folded head weights [2][64], folded head bias [2]
+    for (int l = 0; l < nh; ++l) {
+      float bb = 0.f;
+      if (lane < H) {
+        bb = w.b_hid[l * H + lane];
+        if (bn && l > 0)
+          for (int hi2 = 0; hi2 < H; ++hi2)
+            bb += w.w_hid[(static_cast<size_t>(l) * H + hi2) * H + lane] * w.bn_b[(l - 1) * H + hi2];
+      }
+      cst[l * HP + lane] = bb;
+    }
+    cst[nh * HP + lane] = lane < H ? wt_head(w, H, bn, nh, lane, 0) : 0.f;
+    cst[(nh + 1) * HP + lane] = lane < H ? wt_head(w, H, bn, nh, lane, 1) : 0.f;
+    if (lane < 2) {
+      float bb = w.b_head[lane];
+      if (bn && nh > 0)
+        for (int h = 0; h < H; ++h) bb += w.w_head[h * 2 + lane] * w.bn_b[(nh - 1) * H + h];
+      cst[(nh + 2) * HP + lane] = bb;
+    }
   }
 }
 
@@ -223,32 +251,34 @@ __global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ ds
   dst[i] = h < H ? src[r * H + h] : 0.f;
 }
 
-template <int KB, int JB, int NP>
+template <int NH, int KB, int JB, int NP>
 struct Shared {
-  static constexpr int NFR = n_frags(KB, JB);
+  static constexpr int NFR = n_frags(NH, KB, JB);
   static constexpr int NPL = NP == 3 ? 2 : 1;
+  static constexpr int NCST = (NH + 2) * HP + 4;
   bf8 img[NFR][NPL][64];
-  float cst[3 * HP + 4];
+  float cst[NCST];
 };
 
 // Compiler-only fence: keeps the (loop-invariant) LDS weight-fragment loads next to their
 // use instead of hoisted out of the unit loop with ~100-200 VGPRs live.
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
 
-template <int KB, int JB, int NP>
-__device__ __forceinline__ Fr8<NP> wfrag(const Shared<KB, JB, NP>& sh, int f, int lane) {
+template <int NH, int KB, int JB, int NP>
+__device__ __forceinline__ Fr8<NP> wfrag(const Shared<NH, KB, JB, NP>& sh, int f, int lane) {
   Fr8<NP> r;
   r.h = sh.img[f][0][lane];
   if constexpr (NP == 3) r.l = sh.img[f][1][lane];
   return r;
 }
 
-template <int KB, int JB, int NP>
-__device__ __forceinline__ void load_shared(Shared<KB, JB, NP>& sh, const bf8* __restrict__ img,
+template <int NH, int KB, int JB, int NP>
+__device__ __forceinline__ void load_shared(Shared<NH, KB, JB, NP>& sh, const bf8* __restrict__ img,
                                             const float* __restrict__ cst) {
-  constexpr int N = Shared<KB, JB, NP>::NFR * Shared<KB, JB, NP>::NPL * 64;
+  using SH = Shared<NH, KB, JB, NP>;
+  constexpr int N = SH::NFR * SH::NPL * 64;
   for (int i = threadIdx.x; i < N; i += NT) (&sh.img[0][0][0])[i] = img[i];
-  for (int i = threadIdx.x; i < 3 * HP + 4; i += NT) sh.cst[i] = cst[i];
+  for (int i = threadIdx.x; i < SH::NCST; i += NT) sh.cst[i] = cst[i];
 }
 
 // transposed image: [p = 16 rows][64 h] bf16, 16 chunks of 4 per 128-byte row, chunk XOR row
@@ -338,11 +368,13 @@ __device__ __forceinline__ Fr4<NP> ua_frag(const float* uw, int s, int jb, int g
   return split4<NP>(f4{q[0], q[s], q[2 * s], q[3 * s]});
 }
 
-// forward of one unit from its staged inputs; X[0] holds C + theta on entry.  On return
-// X[0], X[1] hold the layer outputs and mu / rr the head outputs at p = c.
-template <int KB, int JB, int NP>
-__device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<KB, JB, NP>& sh, const float* uw,
-                                             f4 (&X)[2][4], float& mu, float& rr) {
+// forward of one unit from its staged inputs: X holds C + theta on entry and the last layer's
+// ELU output I_NH on return; mu / rr are the head outputs at p = c.  With IMG, the inputs of
+// hidden layers I_0 .. I_{NH-1} (with the ones row 63) are written to images[0 .. NH-1].
+template <int NH, int KB, int JB, int NP, bool IMG>
+__device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB, JB, NP>& sh, const float* uw,
+                                             f4 (&X)[4], float& mu, float& rr, __bf16* const* ih,
+                                             __bf16* const* il) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   f4 acc[4];
 #pragma unroll
@@ -351,46 +383,54 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<KB, JB
   for (int kb = 0; kb < KB; ++kb) {
     const Fr8<NP> uf = u_frag<NP>(uw, a.s, kb, g, c);
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, 16 + kb * 4 + ob, lane), uf, acc[ob]);
+    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, 16 * NH + kb * 4 + ob, lane), uf, acc[ob]);
   }
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[0][rb][r] = elu_fast(acc[rb][r] + X[0][rb][r]);
-  fence();
+    for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast(acc[rb][r] + X[rb][r]);
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int l = 0; l < NH; ++l) {
+    fence();
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const Fr8<NP> xf = chain_frag<NP>(X[0], ks);
+    for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, ob * 2 + ks, lane), xf, acc[ob]);
-  }
+    for (int ks = 0; ks < 2; ++ks) {
+      const Fr8<NP> xf = chain_frag<NP>(X, ks);
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) {
-    const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[16 * rb + 4 * g]);
+      for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, l * 8 + ob * 2 + ks, lane), xf, acc[ob]);
+    }
+    if constexpr (IMG) {
+      // I_l with its ones row (bias gradient of layer l) -> image l
+      if (g == 3) X[3][3] = 1.f;
+      put_image<NP>(ih[l], il[l], X, g, c);
+    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[1][rb][r] = elu_fast(acc[rb][r] + bv[r]);
+    for (int rb = 0; rb < 4; ++rb) {
+      const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[l * HP + 16 * rb + 4 * g]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast(acc[rb][r] + bv[r]);
+    }
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus)
   fence();
-  const int fh = 16 + 4 * KB + 2 * JB;
+  const int fh = 16 * NH + 4 * KB + 2 * JB;
   f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X[1], ks), d);
-  mu = __shfl(d[0], c, 64) + sh.cst[3 * HP + 0];
-  rr = __shfl(d[1], c, 64) + sh.cst[3 * HP + 1];
+  for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X, ks), d);
+  mu = __shfl(d[0], c, 64) + sh.cst[(NH + 2) * HP + 0];
+  rr = __shfl(d[1], c, 64) + sh.cst[(NH + 2) * HP + 1];
 }
 
 // ---------------------------------------------------------------------------
 // forward kernel: one work item (sample group x t-chunk) per wave; samples outer
 // ---------------------------------------------------------------------------
-template <int KB, int JB, int NP>
+template <int NH, int KB, int JB, int NP>
 __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ u_next, float* __restrict__ ls_slab) {
-  __shared__ Shared<KB, JB, NP> sh;
+  __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][UW];
   load_shared(sh, img, cst);
   __syncthreads();
@@ -411,10 +451,10 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
       fence();
       const int nP = min(P, m_hi - m0), t0 = a.s * m0;
-      f4 X[2][4];
+      f4 X[4];
       float mu, rr;
-      load_unit(a, ub, nullptr, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, nullptr, X[0]);
-      unit_forward<KB, JB, NP>(a, sh, uw, X, mu, rr);
+      load_unit(a, ub, nullptr, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, nullptr, X);
+      unit_forward<NH, KB, JB, NP, false>(a, sh, uw, X, mu, rr, nullptr, nullptr);
       if (g == 0 && c < nP) {
         const float sg = softplus_fast(rr) + 1e-10f;
         const int oq = a.s * c + (a.s - 1);
@@ -435,7 +475,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 // backward kernel: one work item per wave; tiles outer, samples inner
 // ---------------------------------------------------------------------------
-template <int KB, int JB, int NP>
+template <int NH, int KB, int JB, int NP>
 __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const float* __restrict__ gout, const float* __restrict__ dls,
@@ -445,8 +485,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
                                                     float* __restrict__ halo) {
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
-  __shared__ Shared<KB, JB, NP> sh;
-  __shared__ __bf16 timg[NW][2][NPL][P * HP];  // [wave][slot][plane][p][h]
+  constexpr int NS = NH + 1;   // images: I_0 .. I_NH (reused for dZ_l and dA0)
+  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ __bf16 timg[NW][NS][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][DTH];
   __shared__ float carry[NW][S][KP];
   __shared__ float gsc[NW][3][P];              // sigma, d r, go even (stride 2)
@@ -470,22 +511,27 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   const int grp = item / a.n_chunks, chn = item % a.n_chunks;
   const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
-  __bf16* xi_h = timg[w][0][0];
-  __bf16* xi_l = timg[w][0][NPL - 1];
-  __bf16* dz_h = timg[w][1][0];
-  __bf16* dz_l = timg[w][1][NPL - 1];
+  __bf16* ih[NS];
+  __bf16* il[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    ih[i] = timg[w][i][0];
+    il[i] = timg[w][i][NPL - 1];
+  }
   float* dsc = &dscr[w][0][0];
   float* mycarry = &carry[w][0][0];
   float* uw = uwin[w];
   float* gw = gwin[w];
-  const float* whmu = &sh.cst[HP];
-  const float* whr = &sh.cst[2 * HP];
+  const float* whmu = &sh.cst[NH * HP];
+  const float* whr = &sh.cst[(NH + 1) * HP];
 
-  f4 dW[4][4], dWe[JB][4], dWh[4];
+  f4 dW[NH][4][4], dWe[JB][4], dWh[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int l = 0; l < NH; ++l)
 #pragma unroll
-    for (int o = 0; o < 4; ++o) dW[i][o] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) dW[l][i][o] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < JB; ++i)
 #pragma unroll
@@ -493,7 +539,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
   for (int i = 0; i < 4; ++i) dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
   const bf4 ones4 = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
-  const int fwc = 16 + 4 * KB, fis = 18 + 4 * KB + 2 * JB;
+  const int fwc = 16 * NH + 4 * KB, fis = 16 * NH + 4 * KB + 2 * JB + 2;
 
   for (int m0 = m_lo; m0 < m_hi; m0 += P) {
     const int nP = min(P, m_hi - m0), t0 = a.s * m0, fin = a.s * nP;
@@ -508,17 +554,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       const int wi = win ? win[b] : 0;
       const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
       const float dl = dls[b];
-      f4 X[2][4];
+      f4 XN[4];
       float mu, rr;
-      load_unit(a, ub, gb, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, gw, X[0]);
-      unit_forward<KB, JB, NP>(a, sh, uw, X, mu, rr);
-      // X0 with its ones row -> image (slot 0) for dW; X1 with its ones row -> slot 1 for dW_head
-      if (g == 3) {
-        X[0][3][3] = 1.f;
-        X[1][3][3] = 1.f;
-      }
-      put_image<NP>(xi_h, xi_l, X[0], g, c);
-      put_image<NP>(dz_h, dz_l, X[1], g, c);
+      load_unit(a, ub, gb, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, gw, XN);
+      unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il);
+      // I_NH (the head input) with its ones row -> image NH, for dW_head
+      if (g == 3) XN[3][3] = 1.f;
+      put_image<NP>(ih[NH], il[NH], XN, g, c);
 
       // ---- head backward (per position p = c, redundant over g) ----
       const int oq = a.s * c + (a.s - 1);
@@ -535,7 +577,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       }
       fence();
       {
-        // dW_head[h][o] += sum_p X1[h][p] G[o][p]: B fragment G[p = 4 g + jj][o = c]
+        // dW_head[h][o] += sum_p I_NH[h][p] G[o][p]: B fragment G[p = 4 g + jj][o = c]
         f4 gv4;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -547,43 +589,48 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const Fr4<NP> gf = split4<NP>(gv4);
         if (!(a.abl & 1))
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(dz_h, dz_l, hb, g, c), gf, dWh[hb]);
+          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(ih[NH], il[NH], hb, g, c), gf, dWh[hb]);
       }
-      // dz1 = (w_mu gmu + w_r gr) * elu'(E1)
+      // dZ_{NH-1} = (w~_mu gmu + w~_r gr) * elu'(I_NH) -> image NH
       f4 D[4];
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const f4 wm = *reinterpret_cast<const f4*>(&whmu[16 * rb + 4 * g]);
         const f4 wr = *reinterpret_cast<const f4*>(&whr[16 * rb + 4 * g]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) D[rb][r] = (wm[r] * gmu + wr[r] * gr) * elu_d(X[1][rb][r]);
+        for (int r = 0; r < 4; ++r) D[rb][r] = (wm[r] * gmu + wr[r] * gr) * elu_d(XN[rb][r]);
       }
-      put_image<NP>(dz_h, dz_l, D, g, c);
-      // dX0 = W dz1 (chain)
-      fence();
-      f4 dX[4];
+      put_image<NP>(ih[NH], il[NH], D, g, c);
+      // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib) dX[ib] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int l = NH - 1; l >= 0; --l) {
+        fence();
+        f4 dX[4];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const Fr8<NP> df = chain_frag<NP>(D, ks);
+        for (int ib = 0; ib < 4; ++ib) dX[ib] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) dX[ib] = mm<NP>(wfrag(sh, 8 + ib * 2 + ks, lane), df, dX[ib]);
-      }
-      // dW1 += X0 dz1^T
-      fence();
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
-      for (int ib = 0; ib < 4 * !(a.abl & 2); ++ib) {
-        const Fr4<NP> xa = tr_frag<NP>(xi_h, xi_l, ib, g, c);
+          for (int ib = 0; ib < 4; ++ib) dX[ib] = mm<NP>(wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane), df, dX[ib]);
+        }
+        fence();
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) dW[ib][ob] = mm<NP>(xa, tr_frag<NP>(dz_h, dz_l, ob, g, c), dW[ib][ob]);
-      }
-      // dA0 = dX0 * elu'(X0) (X0 from its image; row 63 held 1 where dX0 is 0)
+        for (int ib = 0; ib < 4 * !(a.abl & 2); ++ib) {
+          const Fr4<NP> xa = tr_frag<NP>(ih[l], il[l], ib, g, c);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const f4 x0 = get_own<NP>(xi_h, xi_l, rb, g, c);
+          for (int ob = 0; ob < 4; ++ob)
+            dW[l][ib][ob] = mm<NP>(xa, tr_frag<NP>(ih[l + 1], il[l + 1], ob, g, c), dW[l][ib][ob]);
+        }
+        // D <- dZ_{l-1} (or dA0 for l = 0) from I_l (read back from its image; row 63 held 1
+        // where dI is 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) D[rb][r] = dX[rb][r] * elu_d(x0[r]);
+        for (int rb = 0; rb < 4; ++rb) {
+          const f4 x = get_own<NP>(ih[l], il[l], rb, g, c);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) D[rb][r] = dX[rb][r] * elu_d(x[r]);
+        }
+        if (l > 0) put_image<NP>(ih[l], il[l], D, g, c);
       }
       // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]; dC tile += dA0 (identity selection)
       fence();
@@ -599,13 +646,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         for (int o2 = 0; o2 < 2 * !(a.abl & 16); ++o2)
           dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
       }
-      // dA0 -> slot 1; dW_eps and d theta from its position-contracted fragments
-      put_image<NP>(dz_h, dz_l, D, g, c);
+      // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
+      put_image<NP>(ih[1], il[1], D, g, c);
       fence();
       f4 dth4[4] = {};
 #pragma unroll
       for (int hb = 0; hb < 4 * !(a.abl & 4); ++hb) {
-        const Fr4<NP> ta = tr_frag<NP>(dz_h, dz_l, hb, g, c);
+        const Fr4<NP> ta = tr_frag<NP>(ih[1], il[1], hb, g, c);
         dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mm<NP>(ua_frag<NP>(uw, a.s, jb, g, c), ta, dWe[jb][hb]);
@@ -682,9 +729,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][lane];
   }
 
-  // ---- weight-gradient partials of this work item (layout of flow4's n_wgrad) ----
+  // ---- weight-gradient partials of this work item (layout of flow4's n_wgrad; folded-BN form:
+  //      scatter_wgrad_kernel recovers the BN and unfolded weight gradients) ----
   const int H = a.H;
-  const int nW = a.k * H + H * H + 3 * H + 2 * H + 2;
+  const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
   float* ws = dW_slab + static_cast<size_t>(item) * nW;
 #pragma unroll
   for (int jb = 0; jb < JB; ++jb)
@@ -695,21 +743,23 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const int j = 16 * jb + 4 * g + r, h = 16 * hb + c;
         if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r];
       }
-  const int off_w = a.k * H, off_b = off_w + H * H;
+  const int off_w = a.k * H, off_b = off_w + NH * H * H;
 #pragma unroll
-  for (int ib = 0; ib < 4; ++ib)
+  for (int l = 0; l < NH; ++l)
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
+    for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hi = 16 * ib + 4 * g + r, ho = 16 * ob + c;
-        if (ho < H) {
-          if (hi < H) ws[off_w + hi * H + ho] = dW[ib][ob][r];
-          else if (hi == 63) ws[off_b + ho] = dW[ib][ob][r];  // the ones row: bias gradient
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hi = 16 * ib + 4 * g + r, ho = 16 * ob + c;
+          if (ho < H) {
+            if (hi < H) ws[off_w + (l * H + hi) * H + ho] = dW[l][ib][ob][r];
+            else if (hi == 63) ws[off_b + l * H + ho] = dW[l][ib][ob][r];  // the ones row: bias gradient
+          }
         }
-      }
-  for (int i = lane; i < 2 * H; i += 64) ws[off_b + H + i] = 0.f;  // bn gamma / beta: no BN here
-  const int off_h = off_b + 3 * H;
+  for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;  // bn: recovered at scatter
+  const int off_h = off_b + 3 * NH * H;
   if (c < 2) {
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb)
@@ -775,8 +825,8 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   Ws t{};
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
   const int NPL = np_of(d) == 3 ? 2 : 1;
-  t.img = reinterpret_cast<bf8*>(take(static_cast<size_t>(n_frags(KB, JB)) * NPL * 64 * sizeof(bf8)));
-  t.cst = reinterpret_cast<float*>(take((3 * HP + 4) * sizeof(float)));
+  t.img = reinterpret_cast<bf8*>(take(static_cast<size_t>(n_frags(d->n_hidden, KB, JB)) * NPL * 64 * sizeof(bf8)));
+  t.cst = reinterpret_cast<float*>(take(((d->n_hidden + 2) * HP + 4) * sizeof(float)));
   t.Cp = reinterpret_cast<float*>(take(static_cast<size_t>(d->n_win) * g.Lh * HP * 4));
   t.thp = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * HP * 4));
   if (!backward) {
@@ -824,23 +874,51 @@ __global__ void reduce_by_window_kernel(const float* __restrict__ slab, const in
   out[static_cast<size_t>(wv) * N + cidx] = s;
 }
 
-__global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowGrads g, int k, int H, int nh) {
-  const int nW = k * H + nh * H * H + 3 * nh * H + 2 * H + 2;
+// Scatter the reduced partials into the caller's gradient buffers, undoing the BN folding:
+// for a layer fed by BN (gamma', beta) the kernel accumulated dWE = sum_p E dZ^T and
+// db = sum_p dZ, so  dW = diag(gamma') dWE + beta db^T,  d gamma' = rowsum(W o dWE),
+// d beta = W db  (and d gamma = kBnScale d gamma').  Without BN the partials are the gradients.
+__global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowParams p, VissmFlowGrads g, int k, int H,
+                                     int nh, int bn) {
+  const int off_w = k * H, off_b = off_w + nh * H * H, off_h = off_b + 3 * nh * H;
+  const int nW = off_h + 2 * H + 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nW; i += gridDim.x * blockDim.x) {
     const float v = red[i];
-    int off = 0;
-    if (i < (off += k * H)) { g.w_eps[i] = v; continue; }
-    if (i < off + nh * H * H) { g.w_hid[i - off] = v; continue; }
-    off += nh * H * H;
-    if (i < off + nh * H) { g.b_hid[i - off] = v; continue; }
-    off += nh * H;
-    if (i < off + nh * H) continue;  // bn gamma (no BN on this path)
-    off += nh * H;
-    if (i < off + nh * H) continue;  // bn beta
-    off += nh * H;
-    if (i < off + 2 * H) { g.w_head[i - off] = v; continue; }
-    off += 2 * H;
-    g.b_head[i - off] = v;
+    if (i < off_w) {
+      g.w_eps[i] = v;
+    } else if (i < off_b) {
+      const int r = i - off_w, l = r / (H * H), hi = (r / H) % H, ho = r % H;
+      float x = v;
+      if (bn && l > 0)
+        x = p.bn_g[(l - 1) * H + hi] * kBnScale * v + p.bn_b[(l - 1) * H + hi] * red[off_b + l * H + ho];
+      g.w_hid[r] = x;
+    } else if (i < off_b + nh * H) {
+      g.b_hid[i - off_b] = v;
+    } else if (i < off_h) {
+      // bn gamma (first nh*H) / beta (next nh*H) of layer l: BN_l feeds layer l + 1 or the head
+      const int r = i - off_b - nh * H, which = r / (nh * H), l = (r / H) % nh, h = r % H;
+      if (!bn) continue;
+      float s = 0.f;
+      if (l + 1 < nh) {
+        const float* W = p.w_hid + static_cast<size_t>(l + 1) * H * H;
+        const float* dWE = red + off_w + static_cast<size_t>(l + 1) * H * H;
+        const float* db = red + off_b + (l + 1) * H;
+        for (int o = 0; o < H; ++o) s += W[h * H + o] * (which == 0 ? dWE[h * H + o] : db[o]);
+      } else {
+        for (int o = 0; o < 2; ++o)
+          s += p.w_head[h * 2 + o] * (which == 0 ? red[off_h + h * 2 + o] : red[off_h + 2 * H + o]);
+      }
+      if (which == 0) g.bn_g[l * H + h] = s * kBnScale;
+      else g.bn_b[l * H + h] = s;
+    } else if (i < off_h + 2 * H) {
+      const int r = i - off_h, h = r / 2, o = r % 2;
+      float x = v;
+      if (bn && nh > 0)
+        x = p.bn_g[(nh - 1) * H + h] * kBnScale * v + p.bn_b[(nh - 1) * H + h] * red[off_h + 2 * H + o];
+      g.w_head[r] = x;
+    } else {
+      g.b_head[i - off_h - 2 * H] = v;
+    }
   }
 }
 
@@ -849,9 +927,12 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowGra
 using namespace flow5;
 
 bool flow5_supports(const VissmFlowDesc* d) {
-  // bf16x3 keeps hi and lo images in LDS: k <= 32 there (k <= 64 for bf16)
-  return (d->precision == VISSM_PREC_BF16 || (d->precision == VISSM_PREC_BF16X3 && d->k <= 32)) &&
-         d->n_hidden == 1 && !d->bn && d->H <= DTH && d->k <= 64;
+  // one hidden layer (AR): bf16 and bf16x3 (k <= 32: hi + lo images in LDS); three hidden layers
+  // with or without BN (LV / SV / FHN heads): bf16
+  if (d->H > DTH || d->k > 64) return false;
+  if (d->precision == VISSM_PREC_BF16) return d->n_hidden == 1 || d->n_hidden == 3;
+  if (d->precision == VISSM_PREC_BF16X3) return d->n_hidden == 1 && d->k <= 32;
+  return false;
 }
 
 size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
@@ -859,19 +940,24 @@ size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
   return ws_layout(d, g, backward != 0, nullptr, nullptr);
 }
 
-#define FLOW5_DISPATCH(KERNEL, JB, NP, ...)                                                        \
+#define FLOW5_DISPATCH(KERNEL, NHd, JB, NP, ...)                                                  \
   do {                                                                                             \
     if (NP == 3) {                                                                                 \
+      if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 3>), __VA_ARGS__);                           \
+      else hipLaunchKernelGGL((KERNEL<1, 1, 2, 3>), __VA_ARGS__);                                   \
+    } else if (NHd == 1) {                                                                         \
       switch (JB) {                                                                                \
-        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 3>), __VA_ARGS__); break;                       \
-        default: hipLaunchKernelGGL((KERNEL<1, 2, 3>), __VA_ARGS__); break;                      \
+        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 1>), __VA_ARGS__); break;                       \
+        case 2: hipLaunchKernelGGL((KERNEL<1, 1, 2, 1>), __VA_ARGS__); break;                       \
+        case 3: hipLaunchKernelGGL((KERNEL<1, 2, 3, 1>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<1, 2, 4, 1>), __VA_ARGS__); break;                      \
       }                                                                                            \
     } else {                                                                                       \
       switch (JB) {                                                                                \
-        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1>), __VA_ARGS__); break;                       \
-        case 2: hipLaunchKernelGGL((KERNEL<1, 2, 1>), __VA_ARGS__); break;                       \
-        case 3: hipLaunchKernelGGL((KERNEL<2, 3, 1>), __VA_ARGS__); break;                       \
-        default: hipLaunchKernelGGL((KERNEL<2, 4, 1>), __VA_ARGS__); break;                      \
+        case 1: hipLaunchKernelGGL((KERNEL<3, 1, 1, 1>), __VA_ARGS__); break;                       \
+        case 2: hipLaunchKernelGGL((KERNEL<3, 1, 2, 1>), __VA_ARGS__); break;                       \
+        case 3: hipLaunchKernelGGL((KERNEL<3, 2, 3, 1>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<3, 2, 4, 1>), __VA_ARGS__); break;                      \
       }                                                                                            \
     }                                                                                              \
   } while (0)
@@ -887,8 +973,8 @@ static void launch_pad(const VissmFlowDesc* d, const Geom& g, const float* C, co
 
 static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, hipStream_t st) {
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
-  hipLaunchKernelGGL(prep_kernel, dim3(n_frags(KB, JB)), dim3(64), 0, st, *w, d->H, d->k, np_of(d), KB, JB, ws.img,
-                     ws.cst);
+  hipLaunchKernelGGL(prep_kernel, dim3(n_frags(d->n_hidden, KB, JB)), dim3(64), 0, st, *w, d->H, d->k, d->n_hidden,
+                     d->bn, np_of(d), KB, JB, ws.img, ws.cst);
 }
 
 int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -905,7 +991,7 @@ int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  FLOW5_DISPATCH(fwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst,
+  FLOW5_DISPATCH(fwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst,
                  u_next, ws.ls_slab);
   VISSM_CHECK_LAUNCH("flow5_fwd");
   prof_end(VISSM_PROF_FLOW_FWD, st);
@@ -926,7 +1012,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
-  FLOW5_DISPATCH(bwd_kernel, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next, dlogsig,
+  FLOW5_DISPATCH(bwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next, dlogsig,
                  ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
@@ -951,8 +1037,8 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int nW = n_wgrad(d);
   rc = launch_reduce_rows_inplace(ws.dW_slab, ws.wred, g.n_items, nW, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *gr, d->k,
-                     d->H, d->n_hidden);
+  hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
+                     d->H, d->n_hidden, d->bn);
   VISSM_CHECK_LAUNCH("flow5_scatter");
   return VISSM_OK;
 }
