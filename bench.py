@@ -88,14 +88,84 @@ def cpu_baseline(args, obs, ob, tt):
                       f"T={args.T}, median of {len(steady)} steps after 2 warm-up ({t:.2f} s/step)"}
 
 
+MODEL_DEFAULTS = {  # per-GPU batch, T, kernel_len
+    "ar": (65536, 5000, 8), "sv": (16384, 1508, 50), "lv": (16384, 5000, 20), "fhn": (8192, 2000, 20)}
+
+
+def build_model(args, ctx, dev, prec):
+    """The benchmarked VI_SSM with synthetic data of the configured shape and random-init weights."""
+    from viforssms_amd.vi_ssm import ThetaSpec
+    world = ctx.world
+    p_global = args.B * world
+    common = dict(device=dev, precision=prec, dist=ctx, log_every=10 ** 9)
+    if args.model == "ar":
+        from viforssms_amd.ar import VI_SSM, build_theta_spec
+        from viforssms_amd.data import data_gen
+        # data_gen(5000, 5, 10, [5, .5, 3], 1) after seed(1), as main.py does
+        np.random.seed(1)
+        np.random.seed(1)
+        obs, ob, tt = data_gen(args.T, 5, 10.0, np.array([5.0, 0.5, 3.0]), 1.0, write=False)
+        obs, ob, tt = (np.asarray(a, dtype=np.float32) for a in (obs, ob, tt))
+        theta_spec = build_theta_spec([(0.0, 10.0)] * 3)
+        model = VI_SSM(obs, 1.0, 10.0, theta_spec, [(0.0, 10.0)] * 3, args.T, p_global, args.k, args.T, [50, 50, 50],
+                       3, 10, ob, tt, pre_train=False, learn_rate=1e-3, grad_clip=2.5e8, **common)
+        meta = dict(D=1, nh=1, n_flows=3, ar_data=(obs, ob, tt),
+                    data="synthetic: AR(1) series from data_gen(5000, impute=5, x0=10, theta=[5,.5,3], obs_std=1) "
+                         "after np.random.seed(1); random-init (glorot) weights; base noise from Philox",
+                    workload=f"AR(1) ELBO train step, T=M={args.T}, impute=5, kernel_len={args.k}, no_flows=3, "
+                             f"network_dims=[50,50,50], feat_window=10, B={args.B} trajectories per GPU "
+                             f"(BASELINE batch_dims -> B)")
+    elif args.model == "sv":
+        from viforssms_amd.sv import VI_SSM
+        from viforssms_amd.data import load_sv
+        obs = load_sv()[: args.T + 1]
+        np.random.seed(1)
+        spec = ThetaSpec.build(4, 5, 0.0, 1.0, "relu")
+        model = VI_SSM(obs, -8.5, spec, [(0.0, 10.0)] * 4, 1.0, args.T, p_global, args.k, args.T, [50] * 5, args.T,
+                       5, 5, learn_rate=1e-4, pre_train=False, **common)
+        meta = dict(D=1, nh=3, n_flows=5, data="dat/SV.dat[300:] (the reference's series); random-init weights",
+                    workload=f"SV ELBO train step (SV_dense.py), T=M={args.T}, kernel_len={args.k}, no_flows=5, "
+                             f"network_dims=[50]*5, feat_window=5, B={args.B} per GPU")
+    elif args.model == "lv":
+        from viforssms_amd.lv import VI_SSM, PRIORS
+        from viforssms_amd.data import lv_data_gen
+        obs, ob, tt, _ = lv_data_gen(args.T, dt=0.1, obs_every=100, seed=1)
+        np.random.seed(1)
+        spec = ThetaSpec.build(3, 4, 0.0, 1.0, "elu")
+        model = VI_SSM(obs, ob, tt, np.array([100.0, 100.0]), spec, PRIORS, 0.1, args.T * 0.1, p_global, args.k,
+                       args.T, [50] * 5, args.T, 3, 10, pre_train=False, **common)
+        meta = dict(D=2, nh=3, n_flows=3,
+                    data="synthetic: Euler-Maruyama LV path theta=(0.5,0.0025,0.3), x0=(100,100), dt=0.1, obs N(x,1) "
+                         "every 100 steps; random-init weights",
+                    workload=f"Lotka-Volterra ELBO train step (lotka_volterra_partial.py), T=M={args.T}, "
+                             f"kernel_len={args.k}, no_flows=3, network_dims=[50]*5, feat_window=10, B={args.B} per GPU")
+    else:
+        from viforssms_amd.fhn import VI_SSM
+        from viforssms_amd.data import fhn_data_gen
+        obs, ob, tt, _ = fhn_data_gen(args.T, dt=0.1, obs_every=10, seed=1)
+        np.random.seed(1)
+        spec = ThetaSpec.build(5, 4, 0.0, 1.0, "elu")
+        model = VI_SSM(obs, ob, tt, np.array([2.0, 3.0]), spec, [(0.0, 10.0)] * 5, 0.1, args.T * 0.1, p_global,
+                       args.k, args.T, [50] * 5, args.T, 3, 10, pre_train=False, **common)
+        meta = dict(D=2, nh=3, n_flows=3,
+                    data="synthetic: Euler-Maruyama FHN path, x0=(2,3), dt=0.1, obs N(x,0.1) every 10 steps; "
+                         "random-init weights",
+                    workload=f"FitzHugh-Nagumo ELBO train step (fitz_nag_NVP.py), T=M={args.T}, kernel_len={args.k}, "
+                             f"no_flows=3, network_dims=[50]*5, feat_window=10, B={args.B} per GPU")
+    model.build_flow()
+    return model, meta
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--B", type=int, default=65536, help="trajectories per GPU")
-    ap.add_argument("--T", type=int, default=5000)
-    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--model", choices=["ar", "lv", "sv", "fhn"], default="ar",
+                    help="ar: the BASELINE metric's workload (configs[1]); lv / sv / fhn: configs[2-4] shapes")
+    ap.add_argument("--B", type=int, default=None, help="trajectories per GPU (default per model)")
+    ap.add_argument("--T", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="bf16",
                     help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
                          "reductions and the optimizer are fp32 throughout")
@@ -104,11 +174,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--cpu-min-steps", type=int, default=5)
     args = ap.parse_args()
+    dB, dT, dk = MODEL_DEFAULTS[args.model]
+    args.B = args.B or dB
+    args.T = args.T or dT
+    args.k = args.k or dk
 
     import torch
     from viforssms_amd import _lib
-    from viforssms_amd.ar import VI_SSM, build_theta_spec
-    from viforssms_amd.data import data_gen
     from viforssms_amd.launch import init_distributed
 
     ctx = init_distributed()
@@ -116,17 +188,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     prec = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}[args.precision]
 
-    # synthetic data of the configured shape: data_gen(5000, 5, 10, [5, .5, 3], 1) after seed(1)
-    np.random.seed(1)
-    np.random.seed(1)
-    obs, ob, tt = data_gen(args.T, 5, 10.0, np.array([5.0, 0.5, 3.0]), 1.0, write=False)
-    obs, ob, tt = (np.asarray(a, dtype=np.float32) for a in (obs, ob, tt))
-    theta_spec = build_theta_spec([(0.0, 10.0)] * 3)
-    p_global = args.B * world
-    model = VI_SSM(obs, 1.0, 10.0, theta_spec, [(0.0, 10.0)] * 3, args.T, p_global, args.k, args.T, [50, 50, 50], 3,
-                   10, ob, tt, pre_train=False, learn_rate=1e-3, grad_clip=2.5e8, device=dev, precision=prec,
-                   dist=ctx, log_every=10 ** 9)
-    model.build_flow()
+    model, meta = build_model(args, ctx, dev, prec)
     lib = _lib.load()
 
     def step(i):
@@ -165,11 +227,11 @@ def main():
 
     if rank != 0:
         return
-    B, T, k, H, nh = args.B, args.T, args.k, 50, 1
-    kext = 3 * k + T + 1
-    Lh = [kext - i * k - k for i in range(3)]
+    B, T, k, H, nh, nf, D = args.B, args.T, args.k, 50, meta["nh"], meta["n_flows"], meta["D"]
+    kext = nf * k + D * T + D
+    Lh = [(kext - i * k - k) // D for i in range(nf)]
     fl_pos = flow_bwd_flops_per_position(k, H, nh)
-    flops_per_launch = B * fl_pos * sum(Lh) / 3.0
+    flops_per_launch = B * fl_pos * sum(Lh) / nf
     avg_launch_s = bwd_ms / max(bwd_n, 1) / 1e3
     achieved = flops_per_launch / avg_launch_s / 1e12 if bwd_n else None
     peak = PEAKS_TFLOPS[args.precision]
@@ -177,7 +239,7 @@ def main():
     traffic = measured_traffic(args)
     value = world * B * T * args.steps / elapsed
     res = {
-        "metric": METRIC,
+        "metric": METRIC if args.model == "ar" else METRIC.replace("AR(1) T=5000", f"{args.model.upper()} T={T}"),
         "value": value,
         "unit": "transitions/s",
         "n_gpus": world,
@@ -188,11 +250,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic: AR(1) series from data_gen(5000, impute=5, x0=10, theta=[5,.5,3], obs_std=1) after "
-                "np.random.seed(1); random-init (glorot) weights; base noise from Philox",
-        "config": {"workload": f"AR(1) ELBO train step, T=M={T}, impute=5, kernel_len={k}, no_flows=3, "
-                               f"network_dims=[50,50,50], feat_window=10, B={B} trajectories per GPU "
-                               f"(BASELINE batch_dims -> B)", "global_batch": B * world, "seq_len": T,
+        "data": meta["data"],
+        "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": T,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
@@ -200,8 +259,8 @@ def main():
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }
-    if args.cpu_baseline == "auto" and world == 1:
-        res["cpu_baseline"] = cpu_baseline(args, obs, ob, tt)
+    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
+        res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
     else:
         res["cpu_baseline"] = None
     print(json.dumps(res), flush=True)
