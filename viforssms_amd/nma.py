@@ -132,12 +132,18 @@ class IAF:
         return h
 
     def conv_shared(self, F: torch.Tensor, Lh: int, s: int) -> torch.Tensor:
-        """C[w, m, :] = conv_b + sum_j F[w, s m + j, :] @ conv_w[j, 1:, :]  (valid conv over the features)."""
+        """C[w, m, :] = conv_b + sum_j F[w, s m + j, :] @ conv_w[j, 1:, :]  (valid conv over the features).
+
+        One GEMM against all k taps at once, G = F @ [W_0 | ... | W_{k-1}]  ([.., Lf, k H]), then the
+        diagonal gather C[m] = sum_j G[s m + j, j] as a strided view (LV's F is 10061 x 10061: a loop of
+        k sliced matmuls copied a 400 MB strided slice per tap)."""
         W = self._p("conv/kernel")
-        out = self._p("conv/bias").expand(F.shape[0], Lh, -1)
-        for j in range(self.spec.k):
-            out = out + F[:, j:j + s * (Lh - 1) + 1:s, :] @ W[j, 1:, :]
-        return out.contiguous()
+        k, H = self.spec.k, self.spec.H
+        nw, Lf, CF = F.shape
+        Wcat = W[:, 1:, :].permute(1, 0, 2).reshape(CF, k * H)
+        G = torch.matmul(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV): no copy
+        diag = G.as_strided((nw, Lh, k, H), (Lf * k * H, s * k * H, k * H + H, 1))
+        return (diag.sum(2) + self._p("conv/bias")).contiguous()
 
     def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
         t = theta
