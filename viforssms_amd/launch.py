@@ -10,16 +10,20 @@ from .vi_ssm import DistCtx
 
 
 def init_distributed() -> DistCtx:
+    """One process per GPU: rank r -> device LOCAL_RANK (mod the visible count, so a one-GPU box can
+    rehearse several ranks), RCCL ("nccl") for GPU tensors unless VISSM_DIST_BACKEND says otherwise
+    (gloo: the CPU tests and the single-GPU multi-rank rehearsal)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()
     if world <= 1:
-        if torch.cuda.is_available():
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        if n_dev > 0:
+            torch.cuda.set_device(local % n_dev)
         return DistCtx()
     import torch.distributed as dist
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        backend = "nccl"
+    if n_dev > 0:
+        torch.cuda.set_device(local % n_dev)
+        backend = os.environ.get("VISSM_DIST_BACKEND", "nccl")
     else:
         backend = "gloo"
     if not dist.is_initialized():
