@@ -184,3 +184,16 @@ def test_full_train_step_matches_oracle():
         checked += int(keep.sum())
         assert np.abs(got[name] - ref)[keep].max(initial=0.0) < 2e-6, name
     assert checked > 1000
+
+
+def test_training_loop_runs_and_logs(tmp_path):
+    """VI_SSM.train (AR.py:240-310): pre-training then ELBO steps with summaries and a checkpoint,
+    then load() restores the flat parameters."""
+    model = build_model("ar", 6, 30, 5, 2, 20, 3, 4, DEV)
+    model.pre_train = True
+    model.train(tensorboard_path=str(tmp_path / "train"), save_path=str(tmp_path / "ck.pt"), max_runs=510,
+                verbose=False)
+    assert not model.pre_train and np.isfinite(model.last["loss/ELBO"])
+    before = model.store.flat.detach().clone()
+    model.load(str(tmp_path / "ck.pt"))
+    assert model.store.flat.shape == before.shape

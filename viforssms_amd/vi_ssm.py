@@ -208,7 +208,7 @@ class VISSMBase:
         if "global_norm" in out:
             vals["optimize/global_norm"] = out["global_norm"][0]
         keys = list(vals)
-        stacked = torch.stack([v.float().reshape(()) for v in vals.values()])
+        stacked = torch.stack([v.detach().float().reshape(()) for v in vals.values()])
         if self.dist.world > 1:
             stacked = stacked.clone()
             self.dist.all_reduce_(stacked)
