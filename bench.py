@@ -49,7 +49,7 @@ def measured_traffic(args):
     try:
         d = json.load(open(path))
         e = d.get(args.precision)
-        if e and e.get("B") == args.B and e.get("T") == args.T and e.get("k") == args.k:
+        if e and e.get("B") == args.B and e.get("T") == args.T and e.get("k") == args.k and args.M == args.T:
             return e["bytes_per_launch"]
     except (ValueError, KeyError):
         pass
@@ -107,12 +107,12 @@ def build_model(args, ctx, dev, prec):
         obs, ob, tt = data_gen(args.T, 5, 10.0, np.array([5.0, 0.5, 3.0]), 1.0, write=False)
         obs, ob, tt = (np.asarray(a, dtype=np.float32) for a in (obs, ob, tt))
         theta_spec = build_theta_spec([(0.0, 10.0)] * 3)
-        model = VI_SSM(obs, 1.0, 10.0, theta_spec, [(0.0, 10.0)] * 3, args.T, p_global, args.k, args.T, [50, 50, 50],
+        model = VI_SSM(obs, 1.0, 10.0, theta_spec, [(0.0, 10.0)] * 3, args.T, p_global, args.k, args.M, [50, 50, 50],
                        3, 10, ob, tt, pre_train=False, learn_rate=1e-3, grad_clip=2.5e8, **common)
         meta = dict(D=1, nh=1, n_flows=3, ar_data=(obs, ob, tt),
                     data="synthetic: AR(1) series from data_gen(5000, impute=5, x0=10, theta=[5,.5,3], obs_std=1) "
                          "after np.random.seed(1); random-init (glorot) weights; base noise from Philox",
-                    workload=f"AR(1) ELBO train step, T=M={args.T}, impute=5, kernel_len={args.k}, no_flows=3, "
+                    workload=f"AR(1) ELBO train step, T={args.T}, M={args.M}, impute=5, kernel_len={args.k}, no_flows=3, "
                              f"network_dims=[50,50,50], feat_window=10, B={args.B} trajectories per GPU "
                              f"(BASELINE batch_dims -> B)")
     elif args.model == "sv":
@@ -166,6 +166,9 @@ def main():
     ap.add_argument("--B", type=int, default=None, help="trajectories per GPU (default per model)")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--M", type=int, default=None,
+                    help="AR window length (reference batch_dims of AR.main; default M = T, the BASELINE workload; "
+                         "hyperparameters.txt's case is --B 50 --M 50 --k 50)")
     ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="bf16",
                     help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
                          "reductions and the optimizer are fp32 throughout")
@@ -178,6 +181,9 @@ def main():
     args.B = args.B or dB
     args.T = args.T or dT
     args.k = args.k or dk
+    args.M = args.M or args.T
+    if args.model != "ar" and args.M != args.T:
+        ap.error("--M applies to the AR model only")
 
     import torch
     from viforssms_amd import _lib
@@ -227,7 +233,7 @@ def main():
 
     if rank != 0:
         return
-    B, T, k, H, nh, nf, D = args.B, args.T, args.k, 50, meta["nh"], meta["n_flows"], meta["D"]
+    B, T, k, H, nh, nf, D = args.B, args.M, args.k, 50, meta["nh"], meta["n_flows"], meta["D"]
     kext = nf * k + D * T + D
     Lh = [(kext - i * k - k) // D for i in range(nf)]
     fl_pos = flow_bwd_flops_per_position(k, H, nh)
@@ -251,7 +257,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": meta["data"],
-        "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": T,
+        "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": args.T,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
@@ -259,7 +265,7 @@ def main():
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }
-    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
+    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar" and args.M == args.T:
         res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
     else:
         res["cpu_baseline"] = None

@@ -138,6 +138,14 @@ __device__ __forceinline__ Fr8<NP> chain_frag(const f4 (&X)[4], int ks) {
 }
 
 // hidden row of element j of k-step ks in lane group g (the chain k order)
+// Hidden unit h <-> padded row: swap the two 2-bit fields, h = 16a + 4b + c <-> row 16a + 4c + b
+// (an involution; 63 -> 63).  Row 16 rb + 4 g + r sits in register (rb, r) of lane group g, so
+// units fill whole registers: for H <= 50 registers (3, 1..3) hold only padding and the ones row
+// and skip the elementwise work (NR below).
+__host__ __device__ constexpr int swz(int i) { return (i & ~15) | ((i & 3) << 2) | ((i >> 2) & 3); }
+constexpr int kMaxH = 50;  // units fit rows 0..47 and 48, 52 (dthl keeps DTH = 56 rows)
+constexpr int NR = 13;     // registers (rb, r) with 4 rb + r < NR carry units
+
 __host__ __device__ __forceinline__ int hperm(int ks, int g, int j) {
   return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
 }
@@ -199,6 +207,20 @@ __device__ __forceinline__ float wt_head(const VissmFlowParams& w, int H, int bn
   return (bn && nh > 0) ? x * w.bn_g[(nh - 1) * H + h] * kBnScale : x;
 }
 
+// folded hidden bias b~_l[hout] = b_l + W_l^T beta_{l-1} and head bias (BN after the previous layer)
+__device__ __forceinline__ float bias_hid(const VissmFlowParams& w, int H, int bn, int l, int hout) {
+  float bb = w.b_hid[l * H + hout];
+  if (bn && l > 0)
+    for (int hi = 0; hi < H; ++hi) bb += w.w_hid[(static_cast<size_t>(l) * H + hi) * H + hout] * w.bn_b[(l - 1) * H + hi];
+  return bb;
+}
+__device__ __forceinline__ float bias_head(const VissmFlowParams& w, int H, int bn, int nh, int o) {
+  float bb = w.b_head[o];
+  if (bn && nh > 0)
+    for (int h = 0; h < H; ++h) bb += w.w_head[h * 2 + o] * w.bn_b[(nh - 1) * H + h];
+  return bb;
+}
+
 __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int NP, int KB, int JB,
                             bf8* __restrict__ img, float* __restrict__ cst) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
@@ -207,25 +229,27 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
   for (int j = 0; j < 8; ++j) {
     float x = 0.f;
     int r = f;
-    if (r < 8 * nh) {  // WF
+    if (r < 8 * nh) {  // WF (row 63 of the input carries ones: the folded bias rides in the MFMA)
       const int l = r >> 3, ob = (r >> 1) & 3, ks = r & 1;
-      const int hin = hperm(ks, g, j), hout = 16 * ob + c;
+      const int hin = swz(hperm(ks, g, j)), hout = swz(16 * ob + c);
       if (hin < H && hout < H) x = wt_hid(w, H, bn, l, hin, hout);
+      else if (hin == HP - 1 && hout < H) x = bias_hid(w, H, bn, l, hout) * kLog2e;
     } else if ((r -= 8 * nh) < 8 * nh) {  // WB
       const int l = r >> 3, ib = (r >> 1) & 3, ks = r & 1;
-      const int hin = 16 * ib + c, hout = hperm(ks, g, j);
+      const int hin = swz(16 * ib + c), hout = swz(hperm(ks, g, j));
       if (hin < H && hout < H) x = wt_hid(w, H, bn, l, hin, hout);
     } else if ((r -= 8 * nh) < 4 * KB) {  // WE
       const int kb = r >> 2, ob = r & 3;
-      const int jt = 32 * kb + 8 * g + j, h = 16 * ob + c;
+      const int jt = 32 * kb + 8 * g + j, h = swz(16 * ob + c);
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
     } else if ((r -= 4 * KB) < 2 * JB) {  // WC
       const int jb = r >> 1, ks = r & 1;
-      const int jt = 16 * jb + c, h = hperm(ks, g, j);
+      const int jt = 16 * jb + c, h = swz(hperm(ks, g, j));
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
     } else if ((r -= 2 * JB) < 2) {  // WH
-      const int h = hperm(r, g, j);
+      const int h = swz(hperm(r, g, j));
       if (c < 2 && h < H) x = wt_head(w, H, bn, nh, h, c) * kLn2;
+      else if (c < 2 && h == HP - 1) x = bias_head(w, H, bn, nh, c);
     } else {  // IS
       const int ob = r - 2;
       x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
@@ -241,33 +265,20 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
   if (NPL == 2) img[(f * NPL + 1) * 64 + lane] = lo;
   if (f == 0) {
     // constants: folded biases [nh][64], folded head weights [2][64], folded head bias [2]
-    for (int l = 0; l < nh; ++l) {
-      float bb = 0.f;
-      if (lane < H) {
-        bb = w.b_hid[l * H + lane];
-        if (bn && l > 0)
-          for (int hi2 = 0; hi2 < H; ++hi2)
-            bb += w.w_hid[(static_cast<size_t>(l) * H + hi2) * H + lane] * w.bn_b[(l - 1) * H + hi2];
-      }
-      cst[l * HP + lane] = bb * kLog2e;
-    }
+    const int hu = swz(lane);  // cst rows are padded rows
+    for (int l = 0; l < nh; ++l) cst[l * HP + lane] = hu < H ? bias_hid(w, H, bn, l, hu) * kLog2e : 0.f;
     // folded head weights as bf16 pairs (mu, r) per row h: hi plane, then lo plane (the A
     // fragment of the head backward)
     {
-      const float wm = lane < H ? wt_head(w, H, bn, nh, lane, 0) * kLn2 : 0.f;
-      const float wr = lane < H ? wt_head(w, H, bn, nh, lane, 1) * kLn2 : 0.f;
+      const float wm = hu < H ? wt_head(w, H, bn, nh, hu, 0) * kLn2 : 0.f;
+      const float wr = hu < H ? wt_head(w, H, bn, nh, hu, 1) * kLn2 : 0.f;
       const __bf16 hm = (__bf16)wm, hr = (__bf16)wr;
       const __bf16 lm = (__bf16)(wm - (float)hm), lr = (__bf16)(wr - (float)hr);
       const bf2 ph = {hm, hr}, pl = {lm, lr};
       cst[nh * HP + lane] = __builtin_bit_cast(float, ph);
       cst[(nh + 1) * HP + lane] = __builtin_bit_cast(float, pl);
     }
-    if (lane < 2) {
-      float bb = w.b_head[lane];
-      if (bn && nh > 0)
-        for (int h = 0; h < H; ++h) bb += w.w_head[h * 2 + lane] * w.bn_b[(nh - 1) * H + h];
-      cst[(nh + 2) * HP + lane] = bb;
-    }
+    if (lane < 2) cst[(nh + 2) * HP + lane] = bias_head(w, H, bn, nh, lane);
   }
 }
 
@@ -276,7 +287,7 @@ __global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ ds
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= rows * HP) return;
   const int64_t r = i / HP;
-  const int h = static_cast<int>(i % HP);
+  const int h = swz(static_cast<int>(i % HP));
   dst[i] = h < H ? src[r * H + h] * kLog2e : 0.f;
 }
 
@@ -399,8 +410,9 @@ __device__ __forceinline__ Fr4<NP> ua_frag(const float* uw, int s, int jb, int g
 }
 
 // forward of one unit from its staged inputs: X holds C + theta on entry and the last layer's
-// ELU output I_NH on return; mu / rr are the head outputs at p = c.  With IMG, the inputs of
-// hidden layers I_0 .. I_{NH-1} (with the ones row 63) are written to images[0 .. NH-1].
+// ELU output I_NH (its row 63 set to one) on return; mu / rr are the head outputs at p = c.  The
+// inputs of every product carry ones in row 63, where the fragments hold the (folded, scaled)
+// biases.  With IMG, the hidden layers' inputs I_0 .. I_{NH-1} are written to images[0 .. NH-1].
 template <int NH, int KB, int JB, int NP, bool IMG>
 __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB, JB, NP>& sh, const float* uw,
                                              f4 (&X)[4], float& mu, float& rr, __bf16* const* ih,
@@ -418,10 +430,11 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast<!IMG>(acc[rb][r] + X[rb][r]);
+    for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r] + X[rb][r]) : 0.f;
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     fence();
+    if (g == 3) X[3][3] = 1.f;  // the ones row: bias of layer l (and its gradient)
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -430,26 +443,21 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, l * 8 + ob * 2 + ks, lane), xf, acc[ob]);
     }
-    if constexpr (IMG) {
-      // I_l with its ones row (bias gradient of layer l) -> image l
-      if (g == 3) X[3][3] = 1.f;
-      put_image<NP>(ih[l], il[l], X, g, c);
-    }
+    if constexpr (IMG) put_image<NP>(ih[l], il[l], X, g, c);  // I_l with its ones row -> image l
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const f4 bv = *reinterpret_cast<const f4*>(&sh.cst[l * HP + 16 * rb + 4 * g]);
+    for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[rb][r] = elu_fast<!IMG>(acc[rb][r] + bv[r]);
-    }
+      for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r]) : 0.f;
   }
-  // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus)
+  // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus; bias on the ones row)
   fence();
+  if (g == 3) X[3][3] = 1.f;
   const int fh = 16 * NH + 4 * KB + 2 * JB;
   f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X, ks), d);
-  mu = __shfl(d[0], c, 64) + sh.cst[(NH + 2) * HP + 0];
-  rr = __shfl(d[1], c, 64) + sh.cst[(NH + 2) * HP + 1];
+  mu = __shfl(d[0], c, 64);
+  rr = __shfl(d[1], c, 64);
 }
 
 // ---------------------------------------------------------------------------
@@ -588,7 +596,6 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       load_unit(a, ub, gb, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, gw, XN);
       unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il);
       // I_NH (the head input) with its ones row -> image NH, for dW_head
-      if (g == 3) XN[3][3] = 1.f;
       put_image<NP>(ih[NH], il[NH], XN, g, c);
 
       // ---- head backward (per position p = c, redundant over g) ----
@@ -634,7 +641,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? whp[HP + 16 * rb + c] : 0u, 0u});
           D[rb] = mm<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-          for (int r = 0; r < 4; ++r) D[rb][r] *= elu_d(XN[rb][r]);
+          for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? D[rb][r] * elu_d(XN[rb][r]) : 0.f;
         }
       }
       put_image<NP>(ih[NH], il[NH], D, g, c);
@@ -665,7 +672,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         for (int rb = 0; rb < 4; ++rb) {
           const f4 x = get_own<NP>(ih[l], il[l], rb, g, c);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) D[rb][r] = dX[rb][r] * elu_d(x[r]);
+          for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? dX[rb][r] * elu_d(x[r]) : 0.f;
         }
         if (l > 0) put_image<NP>(ih[l], il[l], D, g, c);
       }
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int h = 16 * rb + 4 * g + r;
+          const int h = swz(16 * rb + 4 * g + r);
           if (h < a.H) dcs[h] = dCa[rb][r] * kLog2e;
         }
     }
@@ -763,7 +770,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
       else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
     }
-    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][lane] * kLog2e;
+    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
   }
 
   // ---- weight-gradient partials of this work item (layout of flow4's n_wgrad; folded-BN form:
@@ -777,7 +784,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int hb = 0; hb < 4; ++hb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = 16 * jb + 4 * g + r, h = 16 * hb + c;
+        const int j = 16 * jb + 4 * g + r, h = swz(16 * hb + c);
         if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r] * kLog2e;
       }
   const int off_w = a.k * H, off_b = off_w + NH * H * H;
@@ -789,7 +796,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int hi = 16 * ib + 4 * g + r, ho = 16 * ob + c;
+          const int hi = swz(16 * ib + 4 * g + r), ho = swz(16 * ob + c);
           if (ho < H) {
             if (hi < H) ws[off_w + (l * H + hi) * H + ho] = dW[l][ib][ob][r];
             else if (hi == 63) ws[off_b + l * H + ho] = dW[l][ib][ob][r] * kLog2e;  // ones row: bias
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int hb = 0; hb < 4; ++hb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int h = 16 * hb + 4 * g + r;
+        const int h = swz(16 * hb + 4 * g + r);
         if (h < H) ws[off_h + h * 2 + c] = dWh[hb][r] * kLn2;
         else if (h == 63) ws[off_h + 2 * H + c] = dWh[hb][r];  // ones row: head bias gradient
       }
@@ -964,7 +971,7 @@ using namespace flow5;
 bool flow5_supports(const VissmFlowDesc* d) {
   // one hidden layer (AR): bf16 and bf16x3 (k <= 32: hi + lo images in LDS); three hidden layers
   // with or without BN (LV / SV / FHN heads): bf16
-  if (d->H > DTH || d->k > 64) return false;
+  if (d->H > kMaxH || d->k > 64) return false;
   if (d->precision == VISSM_PREC_BF16) return d->n_hidden == 1 || d->n_hidden == 3;
   if (d->precision == VISSM_PREC_BF16X3) return d->n_hidden == 1 && d->k <= 32;
   return false;
