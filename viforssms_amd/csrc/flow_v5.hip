@@ -369,29 +369,54 @@ __device__ __forceinline__ Fr4<NP> tr_frag(const __bf16* hi, const __bf16* lo, i
 
 __device__ __forceinline__ int clampi(int i, int n) { return i < n ? i : n - 1; }
 
-// Per-unit inputs, loaded branch-free at the top of the unit: the u window [t0, t0 + 128) and
-// (backward) the upstream-gradient window [t0, t0 + 64) staged in the wave's LDS; C + theta
-// term for the lane's 16 (h, p = c) entries from the zero-padded 64-wide copies (pad_kernel).
-__device__ __forceinline__ void load_unit(const KArgs& a, const float* __restrict__ ub, const float* __restrict__ gb,
-                                          const float* __restrict__ Cw, const float* __restrict__ thb, int m0, int nP,
-                                          int t0, float* uw, float* gw, f4 (&cin)[4]) {
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const float u0 = ub[clampi(t0 + lane, a.L)];
-  const float u1 = ub[clampi(t0 + 64 + lane, a.L)];
-  float gv = 0.f;
+// Per-unit inputs, loaded branch-free: the u window [t0, t0 + 64 WU) and (backward) the
+// upstream-gradient window [t0, t0 + 64), staged in the wave's LDS; C + theta term for the
+// lane's 16 (h, p = c) entries from the zero-padded 64-wide copies (pad_kernel).
+// (positions p >= nP read the last valid row: finite, their outputs are dropped and their
+//  upstream gradient is zero.)  WU = 1 suffices for k <= 32: every read stays below s * 15 + 32.
+template <int WU>
+struct Win {
+  float u[WU];
+  float gv;
+};
+
+template <int WU>
+__device__ __forceinline__ void fetch_win(const KArgs& a, const float* __restrict__ ub, const float* __restrict__ gb,
+                                          int t0, Win<WU>& wn) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < WU; ++i) wn.u[i] = ub[clampi(t0 + 64 * i + lane, a.L)];
+  wn.gv = 0.f;
   if (gb) {
     const int o = t0 + lane;
-    gv = gb[clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
+    wn.gv = gb[clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
   }
+}
+
+template <int WU>
+__device__ __forceinline__ void stage_win(const Win<WU>& wn, float* uw, float* gw) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < WU; ++i) uw[64 * i + lane] = wn.u[i];
+  if (gw) gw[lane] = wn.gv;
+}
+
+__device__ __forceinline__ void load_ct(const float* __restrict__ Cw, const float* __restrict__ thb, int m0, int nP,
+                                        f4 (&cin)[4]) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const f4* crow = reinterpret_cast<const f4*>(Cw + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
   const f4* trow = reinterpret_cast<const f4*>(thb) + g;
-  // (positions p >= nP read the last valid row: finite, their outputs are dropped and their
-  //  upstream gradient is zero)
+  f4 cr[4], tr[4];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) cin[rb] = crow[4 * rb] + trow[4 * rb];
-  uw[lane] = u0;
-  uw[64 + lane] = u1;
-  if (gb) gw[lane] = gv;
+  for (int rb = 0; rb < 4; ++rb) {
+    cr[rb] = crow[4 * rb];
+    tr[rb] = trow[4 * rb];
+  }
+  // all eight loads in flight before the first use (left alone, the scheduler may pair them with
+  // a full vmcnt(0) drain each to save registers)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) cin[rb] = cr[rb] + tr[rb];
 }
 
 // layer-0 B fragment: U[j = 32 kb + 8 g + jj][p = c] = u[t0 + s c + j] (weights are zero for j >= k)
@@ -473,7 +498,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
   load_shared(sh, img, cst);
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int item = blockIdx.x * NW + w;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
   if (item >= a.n_items) return;
   const int grp = item / a.n_chunks, ch = item % a.n_chunks;
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
@@ -491,7 +516,12 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
       const int nP = min(P, m_hi - m0), t0 = a.s * m0;
       f4 X[4];
       float mu, rr;
-      load_unit(a, ub, nullptr, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, nullptr, X);
+      {
+        Win<KB> wn;
+        fetch_win<KB>(a, ub, nullptr, t0, wn);
+        load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, X);
+        stage_win<KB>(wn, uw, nullptr);
+      }
       unit_forward<NH, KB, JB, NP, false>(a, sh, uw, X, mu, rr, nullptr, nullptr);
       if (g == 0 && c < nP) {
         const float sg = softplus_fast(rr) + 1e-10f;
@@ -544,7 +574,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int i = threadIdx.x; i < NW * KP * QW; i += NT) (&dscr[0][0][0])[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int item = blockIdx.x * NW + w;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
   if (item >= a.n_items) return;  // no block-level synchronisation below this point
   const int grp = item / a.n_chunks, chn = item % a.n_chunks;
   const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
@@ -586,14 +616,17 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int bl = 0; bl < nb; ++bl) {
       fence();
       const int b = b_lo + bl;
-      const float* ub = u + static_cast<size_t>(b) * a.L;
-      const float* gb = gout + static_cast<size_t>(b) * a.Lout;
       const int wi = win ? win[b] : 0;
       const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
       const float dl = dls[b];
       f4 XN[4];
       float mu, rr;
-      load_unit(a, ub, gb, Cw, tht + static_cast<size_t>(b) * HP, m0, nP, t0, uw, gw, XN);
+      {
+        Win<KB> wn;
+        fetch_win<KB>(a, u + static_cast<size_t>(b) * a.L, gout + static_cast<size_t>(b) * a.Lout, t0, wn);
+        load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, XN);
+        stage_win<KB>(wn, uw, gw);
+      }
       unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il);
       // I_NH (the head input) with its ones row -> image NH, for dW_head
       put_image<NP>(ih[NH], il[NH], XN, g, c);
@@ -720,7 +753,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       {
         float* db = du + static_cast<size_t>(b) * a.L;
-        for (int base = 0; base < (kAbl & 8 ? 0 : fin + a.k); base += 64) {
+        // fin + k <= 64 when PADDED (k <= 32), <= 96 otherwise
+        constexpr int NBASE = PADDED ? 1 : 2;
+        const int lim = kAbl & 8 ? 0 : fin + a.k;
+#pragma unroll
+        for (int it = 0; it < NBASE; ++it) {
+          const int base = 64 * it;
+          if (base >= lim) break;
           const int q = base + lane;
           float v = 0.f;
           if constexpr (PADDED) {
