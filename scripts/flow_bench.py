@@ -49,8 +49,17 @@ def main():
     import dataclasses
     res = {}
     outs = {}
+    kern = {}  # kernel-only times (HIP events around the flow kernel launches, vissm_profile_*)
+
+    def prof_read(which):
+        tot, cnt = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(lib.vissm_profile_read(which, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
+        return tot.value, cnt.value
+
     for rd in range(args.rounds):
         for im in impls:
+            lib.vissm_profile_reset()
+            lib.vissm_profile_enable(1 if rd > 0 else 0)
             shp = sh
             if im in PREC:
                 shp = dataclasses.replace(sh, precision=PREC[im])
@@ -68,6 +77,10 @@ def main():
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             res.setdefault(im, []).append((t1 - t0, t2 - t1))
+            lib.vissm_profile_enable(0)
+            if rd > 0:
+                (fk, fn), (bk, bn) = prof_read(_lib.PROF_FLOW_FWD), prof_read(_lib.PROF_FLOW_BWD)
+                kern.setdefault(im, []).append((fk / max(fn, 1), bk / max(bn, 1)))
             if rd == 0:
                 outs[im] = [un.detach(), ls.detach()] + [t.grad for t in ins]
     summary = {}
@@ -75,6 +88,11 @@ def main():
         f = sorted(x[0] for x in v[1:] or v)
         b = sorted(x[1] for x in v[1:] or v)
         summary[im] = {"fwd_ms": 1e3 * f[len(f) // 2], "bwd_ms": 1e3 * b[len(b) // 2]}
+        if im in kern:
+            kf = sorted(x[0] for x in kern[im])
+            kb = sorted(x[1] for x in kern[im])
+            summary[im]["fwd_kernel_ms"] = kf[len(kf) // 2]
+            summary[im]["bwd_kernel_ms"] = kb[len(kb) // 2]
     if len(outs) > 1:
         ks = sorted(outs, key=str)
         a0 = outs[ks[0]]
