@@ -27,12 +27,59 @@ from . import _lib
 from .ops import FlowShape, ma_flow, normal_base, base_logprob, elbo_terms, ElboFeeds, AdamaxKernel
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
+from .linalg import linear, tn_split_k
 
 LOG_2PI = math.log(2 * math.pi)
 
 
 def elu(x):
     return torch.nn.functional.elu(x)
+
+
+class _ThetaBranch(torch.autograd.Function):
+    """theta_term = ((theta W0 + b0) W1 + b1) W2 + b2 — the reference's three linear dense layers
+    (AR.py:63-68) — evaluated as one [B, P] x [P, H] product with the collapsed weights.  Every
+    gradient follows from S = theta^T d and s = sum_b d (d = d theta_term), so the backward has
+    no [B, H] intermediates and no K = B weight GEMMs besides S."""
+
+    @staticmethod
+    def forward(ctx, theta, W0, b0, W1, b1, W2, b2):
+        W12 = W1 @ W2
+        ctx.save_for_backward(theta, W0, b0, W1, b1, W2, W12)
+        return torch.addmm(b0 @ W12 + b1 @ W2 + b2, theta, W0 @ W12)
+
+    @staticmethod
+    def backward(ctx, d):
+        theta, W0, b0, W1, b1, W2, W12 = ctx.saved_tensors
+        d = d.contiguous()
+        S = tn_split_k(theta.contiguous(), d)      # theta^T d      [P, H]
+        s = d.sum(0)                                # sum_b d        [H]
+        SW2, sW2 = S @ W2.t(), s @ W2.t()           # through layer 2: theta^T dh1, sum dh1
+        dW2 = (W0 @ W1).t() @ S + torch.outer(b0 @ W1 + b1, s)   # h1^T d, h1 = theta W0 W1 + b0 W1 + b1
+        dW1 = W0.t() @ SW2 + torch.outer(b0, sW2)               # h0^T dh1, h0 = theta W0 + b0
+        dW0 = SW2 @ W1.t()                                      # theta^T dh0, dh0 = dh1 W1^T
+        dtheta = d @ (W0 @ W12).t()
+        return dtheta, dW0, sW2 @ W1.t(), dW1, sW2, dW2, s
+
+
+class _DiagSum(torch.autograd.Function):
+    """C[w, m, :] = sum_j G[w, s m + j, j, :] (the valid conv's diagonal gather).  The backward
+    writes dC into the (non-overlapping) diagonal of a zero dG with one strided copy instead of
+    as_strided's generic accumulate-scatter (an index sort + atomics)."""
+
+    @staticmethod
+    def forward(ctx, G, Lh, s):
+        nw, Lf, k, H = G.shape
+        ctx.meta = (G.shape, Lh, s)
+        return G.as_strided((nw, Lh, k, H), (Lf * k * H, s * k * H, k * H + H, 1)).sum(2)
+
+    @staticmethod
+    def backward(ctx, dC):
+        (nw, Lf, k, H), Lh, s = ctx.meta
+        dG = torch.zeros((nw, Lf, k, H), dtype=dC.dtype, device=dC.device)
+        dG.as_strided((nw, Lh, k, H), (Lf * k * H, s * k * H, k * H + H, 1)).copy_(
+            dC.unsqueeze(2).expand(nw, Lh, k, H))
+        return dG, None, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -126,7 +173,7 @@ class IAF:
         else:
             h = ts[:, :-1, :]
         for j in range(4):
-            h = elu(h @ self._p(f"feat{j}/kernel") + self._p(f"feat{j}/bias"))
+            h = elu(linear(h, self._p(f"feat{j}/kernel"), self._p(f"feat{j}/bias")))
         if f == "lv":                                              # lotka_volterra_partial.py:75-76
             h = h.transpose(1, 2)
         return h
@@ -141,15 +188,13 @@ class IAF:
         k, H = self.spec.k, self.spec.H
         nw, Lf, CF = F.shape
         Wcat = W[:, 1:, :].permute(1, 0, 2).reshape(CF, k * H)
-        G = torch.matmul(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV): no copy
-        diag = G.as_strided((nw, Lh, k, H), (Lf * k * H, s * k * H, k * H + H, 1))
-        return (diag.sum(2) + self._p("conv/bias")).contiguous()
+        G = linear(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV): no copy
+        return (_DiagSum.apply(G.contiguous(), Lh, s) + self._p("conv/bias")).contiguous()
 
     def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
-        t = theta
-        for j in range(3):
-            t = t @ self._p(f"theta{j}/kernel") + self._p(f"theta{j}/bias")
-        return t.contiguous()
+        p = self._p
+        return _ThetaBranch.apply(theta, p("theta0/kernel"), p("theta0/bias"), p("theta1/kernel"),
+                                  p("theta1/bias"), p("theta2/kernel"), p("theta2/bias")).contiguous()
 
     # ---- per-transition part (HIP) ----
     def flow(self, shape: FlowShape, win, u, C, theta_term):

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from .params import ParamStore, glorot_normal
+from .linalg import linear
 
 HIDDEN = (5, 5, 5)
 
@@ -78,13 +79,23 @@ class ThetaFlow:
             self._masks = [torch.tensor(m, dtype=torch.float32, device=device) for m in self.masks_np]
         return self._masks
 
+    def _perm_matrix(self, i: int, z: torch.Tensor) -> torch.Tensor:
+        """one-hot [P, P] with (z @ M)[..., d] = z[..., perms[i][d]]"""
+        key = (i, z.device, z.dtype)
+        cache = self.__dict__.setdefault("_pm", {})
+        if key not in cache:
+            m = torch.zeros(self.P, self.P, dtype=z.dtype, device=z.device)
+            m[self.perms[i], torch.arange(self.P)] = 1.0
+            cache[key] = m
+        return cache[key]
+
     def _shift_log_scale(self, i: int, z: torch.Tensor):
         masks = self._dev_masks(z.device)
         h = z
         nl = len(masks)
         for j in range(nl):
             w = self.store[f"{self.prefix}/maf{i}/dense{j}/kernel"] * masks[j]
-            h = h @ w + self.store[f"{self.prefix}/maf{i}/dense{j}/bias"]
+            h = linear(h, w, self.store[f"{self.prefix}/maf{i}/dense{j}/bias"])
             if j < nl - 1:
                 h = self.act(h)
         h = h.reshape(*z.shape, 2)
@@ -102,7 +113,7 @@ class ThetaFlow:
             z = (z - shift) * torch.exp(-ls)
             lq = lq + ls.sum(-1)
             if i < self.n - 1:
-                z = z[..., self.perms[i]]
+                z = z @ self._perm_matrix(i, z)  # exact; its backward is a product, not a scatter
         return z, lq
 
     def log_prob(self, theta: torch.Tensor):
