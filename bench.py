@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="bf16",
                     help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
                          "reductions and the optimizer are fp32 throughout")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a captured HIP graph (viforssms_amd.graph; needs warmup >= 3)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-B", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
@@ -199,8 +201,13 @@ def main():
 
     def step(i):
         starts = model.select_windows()
-        batch = model.batch_for(starts)
-        model.elbo_step(batch, i)
+        if args.graph:
+            model.graphed_step(starts, i)
+        else:
+            model.elbo_step(model.batch_for(starts), i)
+
+    if args.graph:
+        args.warmup = max(args.warmup, 3)  # two eager warm-up steps, then the capture
 
     for i in range(args.warmup):
         step(i)
@@ -258,7 +265,7 @@ def main():
         "dtype": args.precision,
         "data": meta["data"],
         "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": args.T,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "hip_graph": bool(args.graph)},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                      "kernel": kernel, "flops_per_launch": flops_per_launch,

@@ -55,6 +55,11 @@ int vissm_version(void);
 int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp,
                       int32_t B, int32_t L, int32_t n_last, void* stream);
 
+/* As vissm_normal_base with the row offset read from device memory (*offset_dev): a captured
+ * HIP graph of the training step advances it on the device between replays. */
+int vissm_normal_base_dev(uint64_t seed, const uint64_t* offset_dev, float* eps, float* base_lp,
+                          int32_t B, int32_t L, int32_t n_last, void* stream);
+
 /* base_lp only, for caller-supplied eps (parity mode). */
 int vissm_base_logprob(const float* eps, float* base_lp, int32_t B, int32_t L,
                        int32_t n_last, void* stream);

@@ -41,7 +41,7 @@ def run(argv=None):
     return ar.main(hp.p, hp.kernel_len, hp.T, hp.batch_dims, hp.network_dims, hp.no_flows, hp.priors,
                    hp.feat_window, hp.x0, hp.obs_std, learn_rate=hp.learn_rate, grad_clip=hp.grad_clip,
                    max_runs=args.steps, precision=prec, dist=ctx, seed=args.seed, pre_train=not args.no_pretrain,
-                   log_every=args.log_every)
+                   log_every=args.log_every, graph=args.graph)
 
 
 if __name__ == "__main__":

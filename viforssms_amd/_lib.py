@@ -54,6 +54,7 @@ SIGNATURES = {
     "vissm_last_error": (ctypes.c_char_p, []),
     "vissm_version": (_i32, []),
     "vissm_normal_base": (_i32, [_u64, _u64, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
+    "vissm_normal_base_dev": (_i32, [_u64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_base_logprob": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_flow_workspace_size": (_size_t, [ctypes.POINTER(FlowDesc), _i32]),
     "vissm_flow_fwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,

@@ -53,7 +53,7 @@ def build_theta_spec(priors) -> ThetaSpec:
 def main(p, kernel_len, T, batch_dims, network_dims, no_flows, priors, feat_window, x0, obs_std, learn_rate=1e-3,
          grad_clip=2.5e8, *, dat_dir: Optional[str] = None, max_runs: Optional[int] = None, device=None,
          precision: int = _lib.VISSM_PREC_FP32, dist: Optional[DistCtx] = None, seed: int = 1,
-         pre_train: bool = True, log_every: int = 1):
+         pre_train: bool = True, log_every: int = 1, graph: bool = False):
     """AR.main (AR.py:364-403): load dat/AR_*, build q(theta), VI_SSM, train."""
     dat_dir = os.getcwd() if dat_dir is None else dat_dir
     obs, obs_bin, time_till = load_ar(dat_dir)
@@ -64,5 +64,5 @@ def main(p, kernel_len, T, batch_dims, network_dims, no_flows, priors, feat_wind
                        log_every=log_every)
     var_model.build_flow()
     var_model.train(tensorboard_path=dat_dir + "/train/", save_path=dat_dir + "/model_saves/AR_save.ckpt",
-                    max_runs=max_runs)
+                    max_runs=max_runs, graph=graph)
     return var_model

@@ -120,6 +120,8 @@ def handle_opts(argv=None):
     parser.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="fp32")
     parser.add_argument("--no-pretrain", action="store_true", help="Skip the 501 pre-training runs")
     parser.add_argument("--log-every", type=int, default=1)
+    parser.add_argument("--graph", action="store_true",
+                        help="Run the ELBO steps as a captured HIP graph (launch-bound small configs)")
     return parser.parse_args(argv)
 
 

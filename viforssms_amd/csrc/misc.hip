@@ -24,11 +24,14 @@ void set_error(const char* fmt, ...) {
 // (column group, row + offset) so the stream is independent of the launch
 // geometry and of how rows are sharded across ranks.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_t offset, float* __restrict__ eps,
-                                                          float* __restrict__ base_lp, int L, int n_last) {
+// (offset_dev: the row offset read from device memory instead, so a captured graph can advance it)
+__global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_t offset,
+                                                          const uint64_t* __restrict__ offset_dev,
+                                                          float* __restrict__ eps, float* __restrict__ base_lp,
+                                                          int L, int n_last) {
   __shared__ double red[4];
   const int b = blockIdx.x;
-  const uint64_t row = offset + static_cast<uint64_t>(b);
+  const uint64_t row = (offset_dev ? *offset_dev : offset) + static_cast<uint64_t>(b);
   const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
   float* out = eps + static_cast<size_t>(b) * L;
   double acc = 0.0;
@@ -234,9 +237,21 @@ int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp
                   L, n_last);
   VISSM_CHECK_ARG(eps && base_lp, "normal_base: null pointer");
   if (B == 0) return VISSM_OK;
-  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, offset, eps, base_lp, L,
-                     n_last);
+  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, offset,
+                     static_cast<const uint64_t*>(nullptr), eps, base_lp, L, n_last);
   VISSM_CHECK_LAUNCH("normal_base");
+  return VISSM_OK;
+}
+
+int vissm_normal_base_dev(uint64_t seed, const uint64_t* offset_dev, float* eps, float* base_lp, int32_t B,
+                          int32_t L, int32_t n_last, void* stream) {
+  VISSM_CHECK_ARG(B >= 0 && L > 0 && n_last >= 0 && n_last <= L, "normal_base_dev: bad shape B=%d L=%d n_last=%d",
+                  B, L, n_last);
+  VISSM_CHECK_ARG(eps && base_lp && offset_dev, "normal_base_dev: null pointer");
+  if (B == 0) return VISSM_OK;
+  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, uint64_t{0}, offset_dev, eps,
+                     base_lp, L, n_last);
+  VISSM_CHECK_LAUNCH("normal_base_dev");
   return VISSM_OK;
 }
 

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import FlowShape, ma_flow, normal_base, base_logprob, elbo_terms, ElboFeeds, AdamaxKernel
+from .ops import FlowShape, ma_flow, normal_base, normal_base_dev, base_logprob, elbo_terms, ElboFeeds, AdamaxKernel
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, tn_split_k
@@ -316,11 +316,18 @@ class Engine:
         return Batch(starts, uniq, t(ts_np), win, feeds, feeds_np)
 
     # ---- random inputs (Philox; keyed by global sample index so sharding is exact) ----
-    def draw(self, step: int, B: int, global_offset: int, B_total: int):
+    def draw(self, step: int, B: int, global_offset: int, B_total: int, row0_dev: Optional[torch.Tensor] = None):
+        """eps [B, kernel_ext] + base log-prob and the q(theta) base draw, Philox rows row0 + b with
+        row0 = step * B_total + global_offset (or read from row0_dev, a device counter a captured
+        graph advances)."""
         md = self.mdef
-        row0 = step * B_total + global_offset
-        eps, base_lp = normal_base(self.seed, row0, B, md.kernel_ext, md.n_logsig, self.device)
-        n, _ = normal_base(self.seed ^ 0x5DEECE66D, row0, B, md.P_theta, 0, self.device)
+        if row0_dev is not None:
+            eps, base_lp = normal_base_dev(self.seed, row0_dev, B, md.kernel_ext, md.n_logsig)
+            n, _ = normal_base_dev(self.seed ^ 0x5DEECE66D, row0_dev, B, md.P_theta, 0)
+        else:
+            row0 = step * B_total + global_offset
+            eps, base_lp = normal_base(self.seed, row0, B, md.kernel_ext, md.n_logsig, self.device)
+            n, _ = normal_base(self.seed ^ 0x5DEECE66D, row0, B, md.P_theta, 0, self.device)
         x0 = n * md.theta_base[1] + md.theta_base[0]
         return eps, base_lp, x0
 
@@ -361,8 +368,12 @@ class Engine:
 
     def prior_logprob(self, theta):
         md = self.mdef
-        mean = torch.tensor([m for m, _ in md.priors], dtype=theta.dtype, device=theta.device)
-        sd = torch.tensor([s for _, s in md.priors], dtype=theta.dtype, device=theta.device)
+        key = (theta.device, theta.dtype)
+        cache = self.__dict__.setdefault("_prior_t", {})
+        if key not in cache:  # device constants made once (no host->device copy inside a captured step)
+            cache[key] = (torch.tensor([m for m, _ in md.priors], dtype=theta.dtype, device=theta.device),
+                          torch.tensor([s for _, s in md.priors], dtype=theta.dtype, device=theta.device))
+        mean, sd = cache[key]
         zz = (theta - mean) / sd
         return (-0.5 * zz * zz - torch.log(sd) - 0.5 * LOG_2PI).sum(-1)
 

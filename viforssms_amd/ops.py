@@ -47,6 +47,19 @@ def normal_base(seed: int, offset: int, B: int, L: int, n_last: int, device) -> 
     return eps, lp
 
 
+def normal_base_dev(seed: int, offset_dev: torch.Tensor, B: int, L: int, n_last: int):
+    """normal_base with the Philox row offset in a device uint64 (int64 storage) tensor."""
+    lib = _lib.load()
+    if not (offset_dev.is_cuda and offset_dev.dtype == torch.int64 and offset_dev.numel() == 1):
+        raise _lib.VissmError("normal_base_dev: offset must be one int64 on the GPU")
+    dev = offset_dev.device
+    eps = torch.empty(B, L, dtype=torch.float32, device=dev)
+    lp = torch.empty(B, dtype=torch.float32, device=dev)
+    check(lib.vissm_normal_base_dev(ctypes.c_uint64(seed & (2 ** 64 - 1)), ptr(offset_dev), ptr(eps), ptr(lp),
+                                    B, L, n_last, _lib.stream_handle(dev)), "vissm_normal_base_dev")
+    return eps, lp
+
+
 def base_logprob(eps: torch.Tensor, n_last: int) -> torch.Tensor:
     lib = _lib.load()
     _require_gpu(eps)

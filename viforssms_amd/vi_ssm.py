@@ -127,31 +127,43 @@ class VISSMBase:
         return b
 
     # ------------------------------------------------------------------ one step
-    def forward(self, batch: Batch, step: int, eps=None, x0_theta=None):
+    def forward(self, batch: Batch, step: int, eps=None, x0_theta=None, row0_dev=None):
         """One ELBO evaluation.  eps / x0_theta inject the randomness (parity tests);
-        otherwise they are drawn from the Philox streams keyed by the global sample index."""
+        otherwise they are drawn from the Philox streams keyed by the global sample index
+        (row0_dev: that index's step base on the device, for a captured step)."""
         base_lp = None
         if eps is None or x0_theta is None:
-            e, blp, x0 = self.engine.draw(step, batch.B, self.dist.rank * self.p_local, self.p)
+            e, blp, x0 = self.engine.draw(step, batch.B, self.dist.rank * self.p_local, self.p, row0_dev)
             if eps is None:
                 eps, base_lp = e, blp
             if x0_theta is None:
                 x0_theta = x0
         return self.engine.forward(batch, eps, base_lp, x0_theta)
 
-    def elbo_step(self, batch: Batch, step: int, eps=None, x0_theta=None, apply: bool = True):
+    def elbo_step(self, batch: Batch, step: int, eps=None, x0_theta=None, apply: bool = True, row0_dev=None):
         """grad of sum(-ELBO) (AR.py:228-229) -> all-reduce -> clip_by_global_norm -> Adamax (AR.py:230-234)."""
         st = self.store
         st.zero_grad()
-        out = self.forward(batch, step, eps, x0_theta)
+        out = self.forward(batch, step, eps, x0_theta, row0_dev)
         loss = (-out["elbo"]).sum()
         loss.backward()
+        del loss
+        # drop the autograd graph now: its parameter-accumulation nodes would otherwise live on into
+        # the next step (and, under graph capture, run on the stream they were created on)
+        out = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
         self._reduce_grads()
         if apply:
             o = self._opt_main
             gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm())
             out["global_norm"] = gn
         return out
+
+    def graphed_step(self, starts: np.ndarray, step: int):
+        """elbo_step for the windows `starts` (all ranks' draws) through the captured graph."""
+        if getattr(self, "_graphed", None) is None:
+            from .graph import GraphedStep
+            self._graphed = GraphedStep(self)
+        return self._graphed.step(starts, step)
 
     def clip_norm(self) -> float:
         return float(self.grad_clip)
@@ -217,8 +229,9 @@ class VISSMBase:
         return {k: float(v) for k, v in zip(keys, host)}
 
     def train(self, tensorboard_path: Optional[str], save_path: Optional[str], max_runs: Optional[int] = None,
-              verbose: bool = True):
-        """VI_SSM.train (AR.py:240-310): endless unless early_stopping / max_runs."""
+              verbose: bool = True, graph: bool = False):
+        """VI_SSM.train (AR.py:240-310): endless unless early_stopping / max_runs.  graph: the ELBO
+        steps after pre-training run as a captured HIP graph (viforssms_amd.graph)."""
         if self._opt_main is None:
             self.build_flow()
         if tensorboard_path:
@@ -231,8 +244,8 @@ class VISSMBase:
         converged = False
         while not converged:
             starts = self.select_windows()
-            batch = self.batch_for(starts)
             if self.pre_train:
+                batch = self.batch_for(starts)
                 if run == 0 and verbose and self.dist.rank == 0:
                     print("Pre-training...")
                 if self.pretrain_step(batch, run):
@@ -241,7 +254,10 @@ class VISSMBase:
                         print("Finished pre-training")
                     run = 0
             else:
-                out = self.elbo_step(batch, self.global_step)
+                if graph:
+                    out = self.graphed_step(starts, self.global_step)
+                else:
+                    out = self.elbo_step(self.batch_for(starts), self.global_step)
                 if run % self.log_every == 0:
                     self.last = self.summaries(out)
                     writer.write(run, self.last)
