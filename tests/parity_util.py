@@ -109,6 +109,27 @@ def _oracle_extra(model, batch, B):
     return ex, inv
 
 
+def oracle_reference(model, batch, eps: torch.Tensor, x0: torch.Tensor):
+    """The float64 oracle's per-sample ELBO and d sum(-ELBO) / d variable (by store name) for the
+    model's current parameters, the batch's windows and the injected eps / theta-base draws."""
+    md = model.mdef
+    B = eps.shape[0]
+    st = model.store
+    spec = bridge.spec_from_mdef(md, B)
+    params = bridge.oracle_params(st.state_numpy(), spec, model.engine.theta_dist.masks_np)
+    inv_ex, inv = _oracle_extra(model, batch, B)
+    ts = torch.tensor(batch.ts.double().cpu().numpy()[inv if batch.win is not None else np.zeros(B, dtype=int)],
+                      dtype=O.DT)
+    leaves = O.param_leaves(params)
+    for t in leaves:
+        t.requires_grad_(True)
+    o = O.elbo(spec, params, model.engine.perms, x0, eps, ts, inv_ex)
+    (-o["elbo"]).sum().backward()
+    ref_g = bridge.oracle_grads_by_name(params, [t.grad if t.grad is not None else torch.zeros_like(t)
+                                                 for t in leaves], spec)
+    return o["elbo"].detach().numpy(), ref_g
+
+
 def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
                     device: str = "cuda:0", T: Optional[int] = None, starts=None, precision: int = 0,
                     seed: int = 3) -> Dict:
@@ -136,19 +157,7 @@ def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n
                  for n, (a, s) in st.offsets.items()}
 
     # ---- oracle (CPU float64) ----
-    spec = bridge.spec_from_mdef(md, B)
-    params = bridge.oracle_params(st.state_numpy(), spec, model.engine.theta_dist.masks_np)
-    inv_ex, inv = _oracle_extra(model, batch, B)
-    ts = torch.tensor(batch.ts.double().cpu().numpy()[inv if batch.win is not None else np.zeros(B, dtype=int)],
-                      dtype=O.DT)
-    leaves = O.param_leaves(params)
-    for t in leaves:
-        t.requires_grad_(True)
-    o = O.elbo(spec, params, model.engine.perms, x0, eps, ts, inv_ex)
-    (-o["elbo"]).sum().backward()
-    ref_g = bridge.oracle_grads_by_name(params, [t.grad if t.grad is not None else torch.zeros_like(t)
-                                                 for t in leaves], spec)
-    elbo_ref = o["elbo"].detach().numpy()
+    elbo_ref, ref_g = oracle_reference(model, batch, eps, x0)
 
     elbo_err = float(np.max(np.abs(elbo_gpu - elbo_ref) / np.maximum(np.abs(elbo_ref), 1e-6)))
     gref = np.concatenate([ref_g[n].ravel() for n in st.names()])
