@@ -60,12 +60,14 @@ def cpu_baseline(args, obs, ob, tt):
     """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories."""
     import torch
     from oracle import nma_oracle as O
-    B = args.cpu_B
-    spec = O.ModelSpec(family="ar", p=B, M=args.T, k=args.k, n_flows=3, H=50, n_layers=3, C_time=14, P_theta=3,
+    B = min(args.cpu_B, args.B)
+    spec = O.ModelSpec(family="ar", p=B, M=args.M, k=args.k, n_flows=3, H=50, n_layers=3, C_time=14, P_theta=3,
                        target=float(args.T), priors=[(0.0, 10.0)] * 3, base_loc=1.5, base_scale=0.5)
     g = torch.Generator().manual_seed(0)
     params = O.init_params(spec, g, dtype=torch.float32)
-    ts = torch.tensor(O.ar_time_feats(obs, ob, tt, 3, args.k, args.T, 10, args.T, [0] * B), dtype=torch.float32)
+    rs = np.random.RandomState(0)
+    starts = rs.choice(np.arange(0, args.T, args.M), size=B, replace=args.M * B >= args.T).tolist()
+    ts = torch.tensor(O.ar_time_feats(obs, ob, tt, 3, args.k, args.M, 10, args.T, starts), dtype=torch.float32)
     leaves = O.param_leaves(params)
     slots = [(torch.zeros_like(t), torch.zeros_like(t)) for t in leaves]
     perms = [[0, 1, 2], [0, 2, 1], [0, 2, 1], [2, 0, 1]]
@@ -83,9 +85,10 @@ def cpu_baseline(args, obs, ob, tt):
             break
     steady = times[2:] if len(times) > 2 else times
     t = float(np.median(steady))
-    return {"value": B * args.T / t, "unit": "transitions/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": B * args.M / t, "unit": "transitions/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"fp32 CPU restatement of the TF1 step (oracle/nma_oracle.py) on B={B} trajectories x "
-                      f"T={args.T}, median of {len(steady)} steps after 2 warm-up ({t:.2f} s/step)"}
+                      f"M={args.M} (T={args.T}, k={args.k}), median of {len(steady)} steps after 2 warm-up "
+                      f"({t:.2f} s/step)"}
 
 
 MODEL_DEFAULTS = {  # per-GPU batch, T, kernel_len
@@ -272,7 +275,7 @@ def main():
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }
-    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar" and args.M == args.T:
+    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
         res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
     else:
         res["cpu_baseline"] = None
