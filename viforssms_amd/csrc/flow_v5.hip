@@ -303,6 +303,33 @@ struct Shared {
 // Compiler-only fence: keeps the (loop-invariant) LDS weight-fragment loads next to their
 // use instead of hoisted out of the unit loop with ~100-200 VGPRs live.
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
+// the forward kernel's fences (BWD = false) are optional: with its small register footprint the
+// compiler may keep weight fragments in registers across units
+// Forward kernel: the 8 NH + 4 KB + 2 weight fragments it uses live in registers for the whole
+// item (its footprint allows it) and its fences are off; measured 11.8 -> 10.4 ms per AR-cfg
+// launch.  (The backward keeps its fences: ~250 VGPRs leave no room to hoist anything.)
+#ifndef VISSM_FWD_REGW
+#define VISSM_FWD_REGW 1
+#endif
+#ifndef VISSM_FWD_FENCE
+#define VISSM_FWD_FENCE 0
+#endif
+template <bool BWD>
+__device__ __forceinline__ void fence_fwd() {
+  if constexpr (BWD || VISSM_FWD_FENCE) fence();
+}
+#ifndef VISSM_BWD_FENCES
+#define VISSM_BWD_FENCES 0xff
+#endif
+template <int BIT>
+__device__ __forceinline__ void fence_bwd() {
+  if constexpr ((VISSM_BWD_FENCES >> BIT) & 1) fence();
+}
+template <bool BWD, int BIT>
+__device__ __forceinline__ void fence_uf() {
+  if constexpr (BWD) fence_bwd<BIT>();
+  else fence_fwd<false>();
+}
 
 template <int NH, int KB, int JB, int NP>
 __device__ __forceinline__ Fr8<NP> wfrag(const Shared<NH, KB, JB, NP>& sh, int f, int lane) {
@@ -438,11 +465,23 @@ __device__ __forceinline__ Fr4<NP> ua_frag(const float* uw, int s, int jb, int g
 // ELU output I_NH (its row 63 set to one) on return; mu / rr are the head outputs at p = c.  The
 // inputs of every product carry ones in row 63, where the fragments hold the (folded, scaled)
 // biases.  With IMG, the hidden layers' inputs I_0 .. I_{NH-1} are written to images[0 .. NH-1].
-template <int NH, int KB, int JB, int NP, bool IMG>
+// the forward's weight fragments held in registers (forward kernel: WF, WE, WH in that order)
+template <int NH, int KB, int NP>
+struct FwdRegs {
+  static constexpr int N = 8 * NH + 4 * KB + 2;
+  Fr8<NP> f[N];
+};
+
+template <int NH, int KB, int JB, int NP, bool IMG, bool REGW = false>
 __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB, JB, NP>& sh, const float* uw,
                                              f4 (&X)[4], float& mu, float& rr, __bf16* const* ih,
-                                             __bf16* const* il) {
+                                             __bf16* const* il, const FwdRegs<NH, KB, NP>* wr = nullptr) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  // fragment f of the shared image, or its register copy (index i in FwdRegs order)
+  auto W = [&](int f, int i) -> Fr8<NP> {
+    if constexpr (REGW) return wr->f[i];
+    else return wfrag(sh, f, lane);
+  };
   f4 acc[4];
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
@@ -450,7 +489,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   for (int kb = 0; kb < KB; ++kb) {
     const Fr8<NP> uf = u_frag<NP>(uw, a.s, kb, g, c);
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, 16 * NH + kb * 4 + ob, lane), uf, acc[ob]);
+    for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(W(16 * NH + kb * 4 + ob, 8 * NH + kb * 4 + ob), uf, acc[ob]);
   }
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
@@ -458,7 +497,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
     for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r] + X[rb][r]) : 0.f;
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
-    fence();
+    fence_uf<IMG, 6>();
     if (g == 3) X[3][3] = 1.f;  // the ones row: bias of layer l (and its gradient)
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
@@ -466,7 +505,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
     for (int ks = 0; ks < 2; ++ks) {
       const Fr8<NP> xf = chain_frag<NP>(X, ks);
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(wfrag(sh, l * 8 + ob * 2 + ks, lane), xf, acc[ob]);
+      for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(W(l * 8 + ob * 2 + ks, l * 8 + ob * 2 + ks), xf, acc[ob]);
     }
     if constexpr (IMG) put_image<NP>(ih[l], il[l], X, g, c);  // I_l with its ones row -> image l
 #pragma unroll
@@ -475,12 +514,12 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
       for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r]) : 0.f;
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus; bias on the ones row)
-  fence();
+  fence_uf<IMG, 7>();
   if (g == 3) X[3][3] = 1.f;
   const int fh = 16 * NH + 4 * KB + 2 * JB;
   f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) d = mm<NP>(wfrag(sh, fh + ks, lane), chain_frag<NP>(X, ks), d);
+  for (int ks = 0; ks < 2; ++ks) d = mm<NP>(W(fh + ks, 8 * NH + 4 * KB + ks), chain_frag<NP>(X, ks), d);
   mu = __shfl(d[0], c, 64);
   rr = __shfl(d[1], c, 64);
 }
@@ -504,6 +543,19 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
   float* uw = uwin[w];
+#if VISSM_FWD_REGW
+  constexpr bool REGW = true;
+  FwdRegs<NH, KB, NP> wr;
+#pragma unroll
+  for (int i = 0; i < 8 * NH; ++i) wr.f[i] = wfrag(sh, i, lane);
+#pragma unroll
+  for (int i = 0; i < 4 * KB; ++i) wr.f[8 * NH + i] = wfrag(sh, 16 * NH + i, lane);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) wr.f[8 * NH + 4 * KB + i] = wfrag(sh, 16 * NH + 4 * KB + 2 * JB + i, lane);
+#else
+  constexpr bool REGW = false;
+  const FwdRegs<NH, KB, NP> wr{};
+#endif
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     const float* ub = u + static_cast<size_t>(b) * a.L;
@@ -512,7 +564,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
     const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
     float ls = 0.f;
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
-      fence();
+      fence_fwd<false>();
       const int nP = min(P, m_hi - m0), t0 = a.s * m0;
       f4 X[4];
       float mu, rr;
@@ -522,7 +574,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, X);
         stage_win<KB>(wn, uw, nullptr);
       }
-      unit_forward<NH, KB, JB, NP, false>(a, sh, uw, X, mu, rr, nullptr, nullptr);
+      unit_forward<NH, KB, JB, NP, false, REGW>(a, sh, uw, X, mu, rr, nullptr, nullptr, &wr);
       if (g == 0 && c < nP) {
         const float sg = softplus_fast(rr) + 1e-10f;
         const int oq = a.s * c + (a.s - 1);
@@ -614,7 +666,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
     for (int bl = 0; bl < nb; ++bl) {
-      fence();
+      fence_bwd<0>();
       const int b = b_lo + bl;
       const int wi = win ? win[b] : 0;
       const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
@@ -644,7 +696,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         gsc[w][1][c] = gr;
         if (a.s == 2) gsc[w][2][c] = pv ? gw[2 * c] : 0.f;
       }
-      fence();
+      fence_bwd<1>();
       {
         // dW_head[h][o] += sum_p I_NH[h][p] G[o][p]: B fragment G[p = 4 g + jj][o = c]
         f4 gv4;
@@ -681,7 +733,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
 #pragma unroll
       for (int l = NH - 1; l >= 0; --l) {
-        fence();
+        fence_bwd<2>();
         f4 dX[4];
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) dX[ib] = f4{0.f, 0.f, 0.f, 0.f};
@@ -691,7 +743,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
           for (int ib = 0; ib < 4; ++ib) dX[ib] = mm<NP>(wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane), df, dX[ib]);
         }
-        fence();
+        fence_bwd<3>();
 #pragma unroll
         for (int ib = 0; ib < 4 * !(kAbl & 2); ++ib) {
           const Fr4<NP> xa = tr_frag<NP>(ih[l], il[l], ib, g, c);
@@ -710,7 +762,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         if (l > 0) put_image<NP>(ih[l], il[l], D, g, c);
       }
       // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]; dC tile += dA0 (identity selection)
-      fence();
+      fence_bwd<4>();
       f4 dcn[JB];
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb) dcn[jb] = f4{0.f, 0.f, 0.f, 0.f};
@@ -725,7 +777,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       }
       // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(ih[1], il[1], D, g, c);
-      fence();
+      fence_bwd<5>();
       f4 dth4[4] = {};
 #pragma unroll
       for (int hb = 0; hb < 4 * !(kAbl & 4); ++hb) {
