@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "latent-state transitions/sec (batch_dims×T per step), AR(1) T=5000, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3}  # MI355X dense (MI355X_MICROARCH.md);
 # bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak
 
@@ -239,6 +240,12 @@ def main():
     bwd_ms, bwd_n = tot.value, cnt.value
     _lib.check(lib.vissm_profile_read(_lib.PROF_FLOW_FWD, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
     fwd_ms, fwd_n = tot.value, cnt.value
+    stream_ms = {}
+    nbytes = ctypes.c_double()
+    for kind in (_lib.PROF_ELBO_FWD, _lib.PROF_ELBO_BWD, _lib.PROF_NORMAL):
+        _lib.check(lib.vissm_profile_read(kind, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
+        _lib.check(lib.vissm_profile_bytes(kind, ctypes.byref(nbytes)), "profile_bytes")
+        stream_ms[kind] = (tot.value, cnt.value, nbytes.value)
     lib.vissm_profile_reset()
 
     if rank != 0:
@@ -275,6 +282,21 @@ def main():
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }
+    # the HBM-bound streaming kernels of the step: the algorithmic bytes each launch
+    # states (libvissm records them with its HIP events: z read / dz written by the log-density kernels,
+    # eps written by the base-noise kernel) over the live launch time, against the 8 TB/s HBM peak
+    names = {_lib.PROF_ELBO_FWD: "elbo_fwd_kernel (log-densities: reads z)",
+             _lib.PROF_ELBO_BWD: "elbo_bwd_kernel (reads z, writes dz)",
+             _lib.PROF_NORMAL: "normal_base_kernel (Philox base noise: writes eps)"}
+    streaming = []
+    for kind, name in names.items():
+        ms, n, nb = stream_ms[kind]
+        if n and ms > 0:
+            gbs = nb / (ms / 1e3) / 1e9
+            streaming.append({"kernel": name, "bound": "hbm", "bytes_per_launch": nb / n, "avg_launch_ms": ms / n,
+                              "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                              "launches": n})
+    res["streaming_rooflines"] = streaming
     if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
         res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
     else:

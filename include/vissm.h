@@ -206,14 +206,22 @@ int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N,
 /* ---------------------------------------------------------------------------
  * Opt-in kernel timing (for bench.py's live roofline): when enabled, the flow
  * entry points bracket their main kernel with hipEvents on the launch stream.
- * kind: VISSM_PROF_FLOW_FWD / VISSM_PROF_FLOW_BWD.  read() synchronises the
+ * kind: VISSM_PROF_FLOW_FWD / VISSM_PROF_FLOW_BWD (flow kernels),
+ * VISSM_PROF_ELBO_FWD / VISSM_PROF_ELBO_BWD (log-density kernels), VISSM_PROF_NORMAL
+ * (base-noise kernel).  read() synchronises the
  * recorded events and returns the summed milliseconds and the launch count.
  * ------------------------------------------------------------------------- */
 #define VISSM_PROF_FLOW_FWD 0
 #define VISSM_PROF_FLOW_BWD 1
+#define VISSM_PROF_ELBO_FWD 2
+#define VISSM_PROF_ELBO_BWD 3
+#define VISSM_PROF_NORMAL 4
 void vissm_profile_enable(int32_t on);
 int vissm_profile_read(int32_t kind, double* total_ms, int64_t* count);
 void vissm_profile_reset(void);
+/* Summed algorithmic HBM bytes of the recorded launches of `kind` (the streaming kernels
+ * state theirs: ELBO_FWD / ELBO_BWD / NORMAL; 0 for the flow kernels). */
+int vissm_profile_bytes(int32_t kind, double* total_bytes);
 
 #ifdef __cplusplus
 }

@@ -75,9 +75,10 @@ SIGNATURES = {
     "vissm_profile_enable": (None, [_i32]),
     "vissm_profile_read": (_i32, [_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "vissm_profile_reset": (None, []),
+    "vissm_profile_bytes": (_i32, [_i32, ctypes.POINTER(ctypes.c_double)]),
 }
 
-PROF_FLOW_FWD, PROF_FLOW_BWD = 0, 1
+PROF_FLOW_FWD, PROF_FLOW_BWD, PROF_ELBO_FWD, PROF_ELBO_BWD, PROF_NORMAL = 0, 1, 2, 3, 4
 
 
 class VissmError(RuntimeError):

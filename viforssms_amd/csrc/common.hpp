@@ -112,6 +112,6 @@ int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hi
 // opt-in event timing of main kernels (vissm_profile_*)
 bool prof_on();
 void prof_begin(int kind, hipStream_t st);
-void prof_end(int kind, hipStream_t st);
+void prof_end(int kind, hipStream_t st, double bytes = 0.0);
 
 }  // namespace vissm

@@ -219,6 +219,144 @@ __global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// AR(1) streaming path (the BASELINE configs): the same terms as Model<AR> above, laid out for
+// HBM: each thread owns V = 4 consecutive times and reads its z span with one 16-byte load (the
+// rows are only dword-aligned: M + 1 floats per sample), the window's obs / obs_bin with one
+// 16-byte load each, and the two neighbour values as cached dword loads.  Per-sample constants
+// (1/e^th2, 1/obs_std) are hoisted, so a transition costs a handful of FMAs instead of four
+// IEEE divisions, and the constant terms of the log-densities are added once per sample:
+//   sde = -1/2 sum_t z_t^2 + M (-th2 - log(2 pi)/2),  z_t = (x_{t+1} - th1 x_t - th0) e^{-th2}
+//   obs = -1/2 sum_t bin_t zo_t^2 + (sum_t bin_t)(-log sd - log(2 pi)/2),  zo_t = (x_{t+1} - y_t)/sd
+// (AR.py:169-176).  Per-thread partials are fp32 over at most a few chunks, summed in double in
+// a fixed order.
+// ---------------------------------------------------------------------------
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+constexpr int kArV = 4;
+
+__device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
+
+__global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* __restrict__ z,
+                                                          const float* __restrict__ theta, float* __restrict__ sde,
+                                                          float* __restrict__ obs) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, M = a.M;
+  const int w = a.d.win ? a.d.win[b] : 0;
+  const float* zb = z + static_cast<size_t>(b) * (M + 1);
+  const float* yb = a.d.obs + static_cast<size_t>(w) * M;
+  const float* bb = a.d.obs_bin + static_cast<size_t>(w) * M;
+  const float th0 = theta[b * 3 + 0], th1 = theta[b * 3 + 1], th2 = theta[b * 3 + 2];
+  const float is = __expf(-th2), io = 1.f / a.obs_std;
+  float sq = 0.f, so = 0.f, sb = 0.f;
+  // transitions t -> t+1, t in [0, M): full chunks of V, then the tail
+  const int nfull = M / kArV;
+  for (int i = threadIdx.x; i < nfull; i += blockDim.x) {
+    const int t0 = kArV * i;
+    const f4u x = ld4(zb + t0);
+    const float xn = zb[t0 + kArV];
+    const f4u y = ld4(yb + t0), bn = ld4(bb + t0);
+    const float xs[kArV + 1] = {x[0], x[1], x[2], x[3], xn};
+#pragma unroll
+    for (int j = 0; j < kArV; ++j) {
+      const float zt = (xs[j + 1] - th1 * xs[j] - th0) * is;
+      const float zo = (xs[j + 1] - y[j]) * io;
+      sq += zt * zt;
+      so += bn[j] * zo * zo;
+      sb += bn[j];
+    }
+  }
+  for (int t = kArV * nfull + threadIdx.x; t < M; t += blockDim.x) {
+    const float zt = (zb[t + 1] - th1 * zb[t] - th0) * is;
+    const float zo = (zb[t + 1] - yb[t]) * io;
+    sq += zt * zt;
+    so += bb[t] * zo * zo;
+    sb += bb[t];
+  }
+  const double rq = block_sum(static_cast<double>(sq), red);
+  const double ro = block_sum(static_cast<double>(so), red);
+  const double rb = block_sum(static_cast<double>(sb), red);
+  if (threadIdx.x == 0) {
+    sde[b] = static_cast<float>(-0.5 * rq + M * (-static_cast<double>(th2) - 0.5 * kLog2Pi));
+    if (obs) obs[b] = static_cast<float>(-0.5 * ro + rb * (-std::log(static_cast<double>(a.obs_std)) - 0.5 * kLog2Pi));
+  }
+}
+
+// d/dz of gs * sde + go * obs at times t in [0, M], and d/dtheta of gs * sde.  Element t takes the
+// head gradient of transition t (t < M) and the tail gradient of transition t - 1 plus its obs
+// term (t >= 1); each thread recomputes the transition before its chunk instead of exchanging it.
+__global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* __restrict__ z,
+                                                          const float* __restrict__ theta,
+                                                          const float* __restrict__ g_sde,
+                                                          const float* __restrict__ g_obs, float* __restrict__ dz,
+                                                          float* __restrict__ dtheta) {
+  __shared__ double red[4];
+  const int b = blockIdx.x, M = a.M;
+  const int w = a.d.win ? a.d.win[b] : 0;
+  const float* zb = z + static_cast<size_t>(b) * (M + 1);
+  float* dzb = dz + static_cast<size_t>(b) * (M + 1);
+  const float* yb = a.d.obs + static_cast<size_t>(w) * M;
+  const float* bb = a.d.obs_bin + static_cast<size_t>(w) * M;
+  const float th0 = theta[b * 3 + 0], th1 = theta[b * 3 + 1], th2 = theta[b * 3 + 2];
+  const float is = __expf(-th2), io = 1.f / a.obs_std;
+  const float gs = g_sde ? g_sde[b] : 0.f, go = g_obs ? g_obs[b] : 0.f;
+  const float cgh = gs * is * th1, cgt = -gs * is, cgo = -go * io;  // d/dx_t of the three terms per z / zo
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;  // sum_t of z_t, z_t x_t, z_t^2 - 1 over owned transitions
+  // element t, given x_{t-1}, x_t, x_{t+1}: transition t (if t < M) and t - 1 (if t >= 1)
+  auto elem = [&](int t, float xp, float xc, float xn, float y, float bn) -> float {
+    float gx = 0.f;
+    if (t < M) {
+      const float zt = (xn - th1 * xc - th0) * is;
+      gx += cgh * zt;
+      a0 += zt;
+      a1 += zt * xc;
+      a2 += zt * zt - 1.f;
+    }
+    if (t >= 1) {
+      const float zp = (xc - th1 * xp - th0) * is;
+      gx += cgt * zp + cgo * bn * (xc - y) * io;
+    }
+    return gx;
+  };
+  // interior chunks: t0 >= 1 and t0 + V <= M, so x_{t0-1} .. x_{t0+V} and obs[t0-1 .. t0+V-2] exist
+  const int ilo = 1, ihi = M / kArV;  // chunks i in [ilo, ihi)
+  for (int i = ilo + threadIdx.x; i < ihi; i += blockDim.x) {
+    const int t0 = kArV * i;
+    const f4u x = ld4(zb + t0), y = ld4(yb + t0 - 1), bn = ld4(bb + t0 - 1);
+    const float xs[kArV + 2] = {zb[t0 - 1], x[0], x[1], x[2], x[3], zb[t0 + kArV]};
+    f4u g;
+#pragma unroll
+    for (int j = 0; j < kArV; ++j) {
+      // all four elements are interior: t in [1, M)
+      const float zt = (xs[j + 2] - th1 * xs[j + 1] - th0) * is;
+      const float zp = (xs[j + 1] - th1 * xs[j] - th0) * is;
+      g[j] = cgh * zt + cgt * zp + cgo * bn[j] * (xs[j + 1] - y[j]) * io;
+      a0 += zt;
+      a1 += zt * xs[j + 1];
+      a2 += zt * zt - 1.f;
+    }
+    *reinterpret_cast<f4u*>(dzb + t0) = g;
+  }
+  // the rest: t in [0, V) and [V ihi, M]
+  const int nrest = kArV + (M + 1 - kArV * ihi);
+  for (int r = threadIdx.x; r < nrest; r += blockDim.x) {
+    const int t = r < kArV ? r : kArV * ihi + (r - kArV);
+    if (t > M || (r >= kArV && t < kArV)) continue;  // (M < V: the two ranges overlap)
+    const float xc = zb[t];
+    const float xp = t >= 1 ? zb[t - 1] : 0.f, xn = t < M ? zb[t + 1] : 0.f;
+    const float y = t >= 1 ? yb[t - 1] : 0.f, bn = t >= 1 ? bb[t - 1] : 0.f;
+    dzb[t] = elem(t, xp, xc, xn, y, bn);
+  }
+  // dlp/dth0 = sum z/s, dlp/dth1 = sum z x_t / s, dlp/dth2 = sum (z^2 - 1)
+  const double r0 = block_sum(static_cast<double>(a0), red);
+  const double r1 = block_sum(static_cast<double>(a1), red);
+  const double r2 = block_sum(static_cast<double>(a2), red);
+  if (threadIdx.x == 0) {
+    dtheta[b * 3 + 0] = static_cast<float>(gs * is * r0);
+    dtheta[b * 3 + 1] = static_cast<float>(gs * is * r1);
+    dtheta[b * 3 + 2] = static_cast<float>(gs * r2);
+  }
+}
+
 static int check(const VissmElboDesc* d, const VissmElboData* data) {
   VISSM_CHECK_ARG(d && data, "elbo: null desc/data");
   VISSM_CHECK_ARG(d->B >= 0 && d->M >= 1 && d->n_win >= 1, "elbo: bad shape B=%d M=%d n_win=%d", d->B, d->M,
@@ -239,6 +377,13 @@ static int check(const VissmElboDesc* d, const VissmElboData* data) {
       VISSM_CHECK_ARG(false, "elbo: unknown model %d", d->model);
   }
   return VISSM_OK;
+}
+
+static int zlen_of(const VissmElboDesc* d) {
+  return (d->model == VISSM_MODEL_LV || d->model == VISSM_MODEL_FHN) ? 2 * (d->M + 1) : d->M + 1;
+}
+static int theta_len(int model) {
+  return model == VISSM_MODEL_SV ? 4 : (model == VISSM_MODEL_FHN ? 5 : 3);
 }
 
 static Args make(const VissmElboDesc* d, const VissmElboData* data) {
@@ -265,13 +410,17 @@ int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
   dim3 grid(d->B), blk(256);
+  prof_begin(VISSM_PROF_ELBO_FWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_AR>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_fwd_kernel, grid, blk, 0, st, a, z, theta, sde, obs); break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     default: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
   }
   VISSM_CHECK_LAUNCH("elbo_fwd");
+  // algorithmic bytes: z read once, theta read, the per-sample sums written (per-window feeds are
+  // L2-resident and not counted)
+  prof_end(VISSM_PROF_ELBO_FWD, st, 4.0 * d->B * (static_cast<double>(zlen_of(d)) + theta_len(d->model) + 3));
   return VISSM_OK;
 }
 
@@ -285,13 +434,17 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
   dim3 grid(d->B), blk(256);
+  prof_begin(VISSM_PROF_ELBO_BWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_AR>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel, grid, blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     default: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
   }
   VISSM_CHECK_LAUNCH("elbo_bwd");
+  // algorithmic bytes: z read, dz written, theta / dtheta and the upstream gradients
+  prof_end(VISSM_PROF_ELBO_BWD, st,
+           4.0 * d->B * (2.0 * zlen_of(d) + 2 * theta_len(d->model) + 3));
   return VISSM_OK;
 }
 

@@ -41,14 +41,19 @@ __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_
     float r1 = sqrtf(-2.f * logf(u01(r.x))), r2 = sqrtf(-2.f * logf(u01(r.z)));
     float a1 = 6.283185307179586f * u01(r.y), a2 = 6.283185307179586f * u01(r.w);
     float v[4] = {r1 * cosf(a1), r1 * sinf(a1), r2 * cosf(a2), r2 * sinf(a2)};
+    const int j0 = g * 4;
+    if (j0 + 3 < L) {
+      // one 16-byte store (rows are only dword-aligned: L is odd in general)
+      typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+      *reinterpret_cast<f4u*>(out + j0) = f4u{v[0], v[1], v[2], v[3]};
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int j = g * 4 + q;
-      if (j < L) {
-        out[j] = v[q];
-        if (j >= L - n_last) acc += -0.5 * static_cast<double>(v[q]) * v[q];
-      }
+      for (int q = 0; q < 4; ++q)
+        if (j0 + q < L) out[j0 + q] = v[q];
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (j0 + q < L && j0 + q >= L - n_last) acc += -0.5 * static_cast<double>(v[q]) * v[q];
   }
   double s = block_sum(acc, red);
   if (threadIdx.x == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
@@ -196,30 +201,32 @@ __global__ __launch_bounds__(256) void adamax_kernel(float* __restrict__ p, cons
 struct ProfRec {
   int kind;
   hipEvent_t a, b;
+  double bytes;  // algorithmic HBM bytes of the launch (streaming kernels; 0 when not stated)
 };
 static bool g_prof = false;
 static std::mutex g_prof_mu;
 static std::vector<ProfRec> g_prof_recs;
-static thread_local hipEvent_t g_open[2] = {nullptr, nullptr};
+constexpr int kProfKinds = 8;
+static thread_local hipEvent_t g_open[kProfKinds] = {};
 
 bool prof_on() { return g_prof; }
 
 void prof_begin(int kind, hipStream_t st) {
-  if (!g_prof) return;
+  if (!g_prof || kind < 0 || kind >= kProfKinds) return;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   (void)hipEventRecord(e, st);
-  g_open[kind & 1] = e;
+  g_open[kind] = e;
 }
 
-void prof_end(int kind, hipStream_t st) {
-  if (!g_prof || !g_open[kind & 1]) return;
+void prof_end(int kind, hipStream_t st, double bytes) {
+  if (!g_prof || kind < 0 || kind >= kProfKinds || !g_open[kind]) return;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   (void)hipEventRecord(e, st);
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  g_prof_recs.push_back({kind, g_open[kind & 1], e});
-  g_open[kind & 1] = nullptr;
+  g_prof_recs.push_back({kind, g_open[kind], e, bytes});
+  g_open[kind] = nullptr;
 }
 
 }  // namespace vissm
@@ -237,9 +244,11 @@ int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp
                   L, n_last);
   VISSM_CHECK_ARG(eps && base_lp, "normal_base: null pointer");
   if (B == 0) return VISSM_OK;
+  prof_begin(VISSM_PROF_NORMAL, as_stream(stream));
   hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, offset,
                      static_cast<const uint64_t*>(nullptr), eps, base_lp, L, n_last);
   VISSM_CHECK_LAUNCH("normal_base");
+  prof_end(VISSM_PROF_NORMAL, as_stream(stream), 4.0 * B * (static_cast<double>(L) + 1));
   return VISSM_OK;
 }
 
@@ -249,9 +258,11 @@ int vissm_normal_base_dev(uint64_t seed, const uint64_t* offset_dev, float* eps,
                   B, L, n_last);
   VISSM_CHECK_ARG(eps && base_lp && offset_dev, "normal_base_dev: null pointer");
   if (B == 0) return VISSM_OK;
+  prof_begin(VISSM_PROF_NORMAL, as_stream(stream));
   hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, uint64_t{0}, offset_dev, eps,
                      base_lp, L, n_last);
   VISSM_CHECK_LAUNCH("normal_base_dev");
+  prof_end(VISSM_PROF_NORMAL, as_stream(stream), 4.0 * B * (static_cast<double>(L) + 1));
   return VISSM_OK;
 }
 
@@ -335,6 +346,16 @@ int vissm_profile_read(int32_t kind, double* total_ms, int64_t* count) {
   }
   *total_ms = tot;
   *count = n;
+  return VISSM_OK;
+}
+
+int vissm_profile_bytes(int32_t kind, double* total_bytes) {
+  VISSM_CHECK_ARG(total_bytes, "profile_bytes: null pointer");
+  std::lock_guard<std::mutex> lk(vissm::g_prof_mu);
+  double tot = 0.0;
+  for (auto& r : vissm::g_prof_recs)
+    if (r.kind == kind) tot += r.bytes;
+  *total_bytes = tot;
   return VISSM_OK;
 }
 
