@@ -155,6 +155,21 @@ def test_normal_base_statistics_and_logprob():
     assert torch.equal(e2, eps[100:150])
 
 
+@pytest.mark.parametrize("L", [1, 3, 5, 64])
+def test_normal_base_short_rows_same_stream(L):
+    """Rows of <= 64 values (the q(theta) base draws) take the one-thread-per-row kernel: the same
+    Philox stream (keyed by (column group, row)) as the block-per-row kernel, i.e. the first L
+    columns of a long draw, and the same log-density."""
+    from viforssms_amd.ops import normal_base
+    B = 1000
+    long_eps, _ = normal_base(7, 33, B, 1001, 1, DEV)
+    eps, lp = normal_base(7, 33, B, L, L, DEV)
+    assert torch.equal(eps, long_eps[:, :L])
+    e = eps.double()
+    ref = (-0.5 * e ** 2).sum(1) - 0.5 * math.log(2 * math.pi) * L
+    assert torch.allclose(lp.double(), ref, rtol=1e-6, atol=1e-6)
+
+
 def test_full_train_step_matches_oracle():
     """One elbo_step (grad -> clip -> Adamax on the flat buffer) vs oracle.train_step.  Adamax's
     first step moves each variable by lr*0.05*sign(g), so variables whose reference gradient is

@@ -318,6 +318,21 @@ template <bool BWD>
 __device__ __forceinline__ void fence_fwd() {
   if constexpr (BWD || VISSM_FWD_FENCE) fence();
 }
+// backward variants (A/B switches): ELU select as v_med3 in the recompute; dC summed with fp32
+// VALU adds instead of the identity-selection MFMA; per-position LDS writes by every lane instead
+// of a divergent branch (the lanes of a column hold identical values)
+#ifndef VISSM_BWD_MED3
+#define VISSM_BWD_MED3 0
+#endif
+#ifndef VISSM_BWD_VALU_DC
+#define VISSM_BWD_VALU_DC 1
+#endif
+#ifndef VISSM_BWD_KFIX
+#define VISSM_BWD_KFIX 8  // > 0: a straight-line transposed-conv sum when k equals it
+#endif
+#ifndef VISSM_BWD_UNCOND
+#define VISSM_BWD_UNCOND 0
+#endif
 #ifndef VISSM_BWD_FENCES
 #define VISSM_BWD_FENCES 0xff
 #endif
@@ -494,7 +509,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r] + X[rb][r]) : 0.f;
+    for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(acc[rb][r] + X[rb][r]) : 0.f;
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     fence_uf<IMG, 6>();
@@ -511,7 +526,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r]) : 0.f;
+      for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(acc[rb][r]) : 0.f;
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus; bias on the ones row)
   fence_uf<IMG, 7>();
@@ -691,7 +706,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       float dsig = gmu * uw[oq + a.k];
       if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * __frcp_rn(sig);
       const float gr = dsig * sigmoid_fast(rr);
-      if (g == 0) {
+      if (VISSM_BWD_UNCOND || g == 0) {
         gsc[w][0][c] = sig;
         gsc[w][1][c] = gr;
         if (a.s == 2) gsc[w][2][c] = pv ? gw[2 * c] : 0.f;
@@ -771,9 +786,19 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dcn[jb] = mm<NP>(wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
+        if constexpr (!VISSM_BWD_VALU_DC) {
 #pragma unroll
-        for (int o2 = 0; o2 < 2 * !(kAbl & 16); ++o2)
-          dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
+          for (int o2 = 0; o2 < 2 * !(kAbl & 16); ++o2)
+            dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
+        }
+      }
+      if constexpr (VISSM_BWD_VALU_DC) {
+        // dC tile += dA0 (same lane layout): fp32 adds on the unit-carrying registers
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (4 * rb + r < NR) dCa[rb][r] += D[rb][r];
       }
       // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(ih[1], il[1], D, g, c);
@@ -786,7 +811,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mm<NP>(ua_frag<NP>(uw, a.s, jb, g, c), ta, dWe[jb][hb]);
       }
-      if (c == 0) {
+      if (VISSM_BWD_UNCOND || c == 0) {  // (every column of dth4 holds the same sums)
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
           if (16 * hb + 4 * g < DTH) {
@@ -816,8 +841,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           float v = 0.f;
           if constexpr (PADDED) {
             const int qc = q < QW ? q : QW - 1;
+            if (VISSM_BWD_KFIX > 0 && a.k == VISSM_BWD_KFIX) {
+#pragma unroll
+              for (int j = 0; j < (VISSM_BWD_KFIX > 0 ? VISSM_BWD_KFIX : 1); ++j) v += dsc[j * QW + qc];
+            } else {
 #pragma unroll 4
-            for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
+              for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
+            }
           } else {
 #pragma unroll 4
             for (int j = 0; j < a.k; ++j) {
@@ -1145,8 +1175,8 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
-  FLOW5_DISPATCH(bwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next, dlogsig,
-                 ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
+  FLOW5_DISPATCH(bwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next,
+                 dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
   if (g.n_chunks > 1) {

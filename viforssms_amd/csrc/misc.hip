@@ -59,6 +59,46 @@ __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_
   if (threadIdx.x == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
 }
 
+// Short rows (the q(theta) base draws, L = P_theta): one thread per row, the same Philox stream
+// (counter (group, row)) and the same fixed-order sum, without a 256-thread block per row.
+constexpr int kShortRow = 64;
+__global__ __launch_bounds__(256) void normal_base_short_kernel(uint64_t seed, uint64_t offset,
+                                                                const uint64_t* __restrict__ offset_dev,
+                                                                float* __restrict__ eps, float* __restrict__ base_lp,
+                                                                int B, int L, int n_last) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t row = (offset_dev ? *offset_dev : offset) + static_cast<uint64_t>(b);
+  const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  float* out = eps + static_cast<size_t>(b) * L;
+  double acc = 0.0;
+  for (int g = 0; g * 4 < L; ++g) {
+    u4 c{static_cast<uint32_t>(g), 0u, static_cast<uint32_t>(row), static_cast<uint32_t>(row >> 32)};
+    u4 r = philox4x32_10(c, k0, k1);
+    float r1 = sqrtf(-2.f * logf(u01(r.x))), r2 = sqrtf(-2.f * logf(u01(r.z)));
+    float a1 = 6.283185307179586f * u01(r.y), a2 = 6.283185307179586f * u01(r.w);
+    float v[4] = {r1 * cosf(a1), r1 * sinf(a1), r2 * cosf(a2), r2 * sinf(a2)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = g * 4 + q;
+      if (j < L) {
+        out[j] = v[q];
+        if (j >= L - n_last) acc += -0.5 * static_cast<double>(v[q]) * v[q];
+      }
+    }
+  }
+  base_lp[b] = static_cast<float>(acc - 0.5 * kLog2Pi * n_last);
+}
+
+static void launch_normal(uint64_t seed, uint64_t offset, const uint64_t* offset_dev, float* eps, float* base_lp,
+                          int B, int L, int n_last, hipStream_t st) {
+  if (L <= kShortRow)
+    hipLaunchKernelGGL(normal_base_short_kernel, dim3((B + 255) / 256), dim3(256), 0, st, seed, offset, offset_dev, eps,
+                       base_lp, B, L, n_last);
+  else
+    hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, st, seed, offset, offset_dev, eps, base_lp, L, n_last);
+}
+
 __global__ __launch_bounds__(256) void base_logprob_kernel(const float* __restrict__ eps, float* __restrict__ base_lp,
                                                            int L, int n_last) {
   __shared__ double red[4];
@@ -245,8 +285,7 @@ int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp
   VISSM_CHECK_ARG(eps && base_lp, "normal_base: null pointer");
   if (B == 0) return VISSM_OK;
   prof_begin(VISSM_PROF_NORMAL, as_stream(stream));
-  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, offset,
-                     static_cast<const uint64_t*>(nullptr), eps, base_lp, L, n_last);
+  launch_normal(seed, offset, nullptr, eps, base_lp, B, L, n_last, as_stream(stream));
   VISSM_CHECK_LAUNCH("normal_base");
   prof_end(VISSM_PROF_NORMAL, as_stream(stream), 4.0 * B * (static_cast<double>(L) + 1));
   return VISSM_OK;
@@ -259,8 +298,7 @@ int vissm_normal_base_dev(uint64_t seed, const uint64_t* offset_dev, float* eps,
   VISSM_CHECK_ARG(eps && base_lp && offset_dev, "normal_base_dev: null pointer");
   if (B == 0) return VISSM_OK;
   prof_begin(VISSM_PROF_NORMAL, as_stream(stream));
-  hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, as_stream(stream), seed, uint64_t{0}, offset_dev, eps,
-                     base_lp, L, n_last);
+  launch_normal(seed, 0, offset_dev, eps, base_lp, B, L, n_last, as_stream(stream));
   VISSM_CHECK_LAUNCH("normal_base_dev");
   prof_end(VISSM_PROF_NORMAL, as_stream(stream), 4.0 * B * (static_cast<double>(L) + 1));
   return VISSM_OK;
