@@ -183,7 +183,17 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + 
 // b~ = b + W^T beta (head likewise), so the kernels only see ELU outputs E; the BN and
 // unfolded weight gradients are recovered from the reduced sums in scatter_wgrad_kernel.
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * NH + 4 * KB + 2 * JB + 6; }
+// head fragments replicate the two output rows into every lane group (VISSM_HEAD_REP)
+#ifndef VISSM_HEAD_REP
+#define VISSM_HEAD_REP 1
+#endif
+// (the backward sums the dC tile with VALU adds by default: no IS fragments then)
+#ifndef VISSM_BWD_VALU_DC
+#define VISSM_BWD_VALU_DC 1
+#endif
+__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) {
+  return 16 * NH + 4 * KB + 2 * JB + (VISSM_BWD_VALU_DC ? 2 : 6);
+}
 
 // phase-ablation mask for timing experiments (build with -DVISSM_V5_ABLATE=mask; results are
 // then wrong by construction).  A compile-time constant: a runtime mask splits the unit into
@@ -248,8 +258,11 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
     } else if ((r -= 2 * JB) < 2) {  // WH
       const int h = swz(hperm(r, g, j));
-      if (c < 2 && h < H) x = wt_head(w, H, bn, nh, h, c) * kLn2;
-      else if (c < 2 && h == HP - 1) x = bias_head(w, H, bn, nh, c);
+      // output rows o' = 4 q + o (o = 0: mu, 1: sigma) for every q with VISSM_HEAD_REP: each lane
+      // group receives (mu, r) of its column in registers 0, 1 of the head MFMA (no shuffle)
+      const int o = VISSM_HEAD_REP ? (c & 3) : c;
+      if (o < 2 && h < H) x = wt_head(w, H, bn, nh, h, o) * kLn2;
+      else if (o < 2 && h == HP - 1) x = bias_head(w, H, bn, nh, o);
     } else {  // IS
       const int ob = r - 2;
       x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
@@ -323,9 +336,6 @@ __device__ __forceinline__ void fence_fwd() {
 // of a divergent branch (the lanes of a column hold identical values)
 #ifndef VISSM_BWD_MED3
 #define VISSM_BWD_MED3 0
-#endif
-#ifndef VISSM_BWD_VALU_DC
-#define VISSM_BWD_VALU_DC 1
 #endif
 #ifndef VISSM_BWD_KFIX
 #define VISSM_BWD_KFIX 8  // > 0: a straight-line transposed-conv sum when k equals it
@@ -535,15 +545,23 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) d = mm<NP>(W(fh + ks, 8 * NH + 4 * KB + ks), chain_frag<NP>(X, ks), d);
-  mu = __shfl(d[0], c, 64);
-  rr = __shfl(d[1], c, 64);
+  if constexpr (VISSM_HEAD_REP) {
+    mu = d[0];
+    rr = d[1];
+  } else {
+    mu = __shfl(d[0], c, 64);
+    rr = __shfl(d[1], c, 64);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // forward kernel: one work item (sample group x t-chunk) per wave; samples outer
 // ---------------------------------------------------------------------------
 template <int NH, int KB, int JB, int NP>
-__global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+#ifndef VISSM_FWD_OCC
+#define VISSM_FWD_OCC 2
+#endif
+__global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ u_next, float* __restrict__ ls_slab) {
