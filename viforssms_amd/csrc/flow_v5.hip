@@ -340,6 +340,9 @@ __device__ __forceinline__ void fence_fwd() {
 #ifndef VISSM_BWD_KFIX
 #define VISSM_BWD_KFIX 8  // > 0: a straight-line transposed-conv sum when k equals it
 #endif
+#ifndef VISSM_BWD_GIMG
+#define VISSM_BWD_GIMG 1  // one hidden layer: the head gradient rides in the dZ image (no G fragment via LDS)
+#endif
 #ifndef VISSM_BWD_UNCOND
 #define VISSM_BWD_UNCOND 0
 #endif
@@ -639,6 +642,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
   constexpr int NS = NH + 1;   // images: I_0 .. I_NH (reused for dZ_l and dA0)
+  constexpr bool GI = VISSM_BWD_GIMG && NH == 1;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][NS][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][DTH];
@@ -726,11 +730,17 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       const float gr = dsig * sigmoid_fast(rr);
       if (VISSM_BWD_UNCOND || g == 0) {
         gsc[w][0][c] = sig;
-        gsc[w][1][c] = gr;
+        if constexpr (!GI) gsc[w][1][c] = gr;
         if (a.s == 2) gsc[w][2][c] = pv ? gw[2 * c] : 0.f;
       }
       fence_bwd<1>();
-      {
+      // GI: the head gradient G rides in two padding rows of the dZ image (below); the I_NH
+      // fragments of dW_head are read now, before that image overwrites I_NH's slot
+      Fr4<NP> i1f[4];
+      if constexpr (GI) {
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) i1f[hb] = tr_frag<NP>(ih[NH], il[NH], hb, g, c);
+      } else {
         // dW_head[h][o] += sum_p I_NH[h][p] G[o][p]: B fragment G[p = 4 g + jj][o = c]
         f4 gv4;
 #pragma unroll
@@ -761,6 +771,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? D[rb][r] * elu_d(XN[rb][r]) : 0.f;
         }
+        if constexpr (GI) {
+          // padding rows 53, 54 (register (3, 1), (3, 2) of lane group 1): (g_mu, g_r) at p = c.
+          // The dX weights are zero there and dW ignores those rows.
+          D[3][1] = g == 1 ? gmu : 0.f;
+          D[3][2] = g == 1 ? gr : 0.f;
+        }
       }
       put_image<NP>(ih[NH], il[NH], D, g, c);
       // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
@@ -783,6 +799,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob)
             dW[l][ib][ob] = mm<NP>(xa, tr_frag<NP>(ih[l + 1], il[l + 1], ob, g, c), dW[l][ib][ob]);
+        }
+        if constexpr (GI) {
+          // dW_head[h][o] += sum_p I_1[h][p] G[o][p]: B = rows 48..63 of the dZ image, columns
+          // c = 5, 6 of the product hold o = 0, 1 (padding rows 53, 54)
+          const Fr4<NP> gb = tr_frag<NP>(ih[NH], il[NH], 3, g, c);
+          if (!(kAbl & 1))
+#pragma unroll
+            for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], gb, dWh[hb]);
         }
         // D <- dZ_{l-1} (or dA0 for l = 0) from I_l (read back from its image; row 63 held 1
         // where dI is 0)
@@ -943,14 +967,15 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
   for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;  // bn: recovered at scatter
   const int off_h = off_b + 3 * NH * H;
-  if (c < 2) {
+  const int oh = GI ? c - 5 : c;  // output column of dW_head's product -> head output o
+  if (oh == 0 || oh == 1) {
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int h = swz(16 * hb + 4 * g + r);
-        if (h < H) ws[off_h + h * 2 + c] = dWh[hb][r] * kLn2;
-        else if (h == 63) ws[off_h + 2 * H + c] = dWh[hb][r];  // ones row: head bias gradient
+        if (h < H) ws[off_h + h * 2 + oh] = dWh[hb][r] * kLn2;
+        else if (h == 63) ws[off_h + 2 * H + oh] = dWh[hb][r];  // ones row: head bias gradient
       }
   }
 }
