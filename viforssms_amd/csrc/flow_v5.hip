@@ -343,6 +343,12 @@ __device__ __forceinline__ void fence_fwd() {
 #ifndef VISSM_BWD_GIMG
 #define VISSM_BWD_GIMG 1  // one hidden layer: the head gradient rides in the dZ image (no G fragment via LDS)
 #endif
+#ifndef VISSM_BWD_I0REG
+#define VISSM_BWD_I0REG 1  // one hidden layer, bf16: elu'(I_0) from registers instead of reading the image back
+#endif
+#ifndef VISSM_BWD_DTHATOM
+#define VISSM_BWD_DTHATOM 0  // the per-sample d theta sums as no-return LDS adds
+#endif
 #ifndef VISSM_BWD_UNCOND
 #define VISSM_BWD_UNCOND 0
 #endif
@@ -503,7 +509,8 @@ struct FwdRegs {
 template <int NH, int KB, int JB, int NP, bool IMG, bool REGW = false>
 __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB, JB, NP>& sh, const float* uw,
                                              f4 (&X)[4], float& mu, float& rr, __bf16* const* ih,
-                                             __bf16* const* il, const FwdRegs<NH, KB, NP>* wr = nullptr) {
+                                             __bf16* const* il, const FwdRegs<NH, KB, NP>* wr = nullptr,
+                                             u2* i0p = nullptr) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   // fragment f of the shared image, or its register copy (index i in FwdRegs order)
   auto W = [&](int f, int i) -> Fr8<NP> {
@@ -536,6 +543,10 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
       for (int ob = 0; ob < 4; ++ob) acc[ob] = mm<NP>(W(l * 8 + ob * 2 + ks, l * 8 + ob * 2 + ks), xf, acc[ob]);
     }
     if constexpr (IMG) put_image<NP>(ih[l], il[l], X, g, c);  // I_l with its ones row -> image l
+    if (IMG && l == 0 && i0p) {  // the bf16 pairs of I_0 kept in registers as well (hi plane)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) i0p[rb] = u2{cvt2(X[rb][0], X[rb][1]), cvt2(X[rb][2], X[rb][3])};
+    }
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
@@ -643,6 +654,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
   constexpr int NS = NH + 1;   // images: I_0 .. I_NH (reused for dZ_l and dA0)
   constexpr bool GI = VISSM_BWD_GIMG && NH == 1;
+  constexpr bool I0R = VISSM_BWD_I0REG && NH == 1 && NP == 1;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][NS][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][DTH];
@@ -716,7 +728,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, XN);
         stage_win<KB>(wn, uw, gw);
       }
-      unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il);
+      u2 i0p[4];
+      unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il, nullptr, I0R ? i0p : nullptr);
       // I_NH (the head input) with its ones row -> image NH, for dW_head
       put_image<NP>(ih[NH], il[NH], XN, g, c);
 
@@ -812,7 +825,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         // where dI is 0)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const f4 x = get_own<NP>(ih[l], il[l], rb, g, c);
+          f4 x;
+          if constexpr (I0R) {  // I_0 from the registers the forward left (same bf16 values as the image)
+            x = f4{__builtin_bit_cast(float, i0p[rb][0] << 16), __builtin_bit_cast(float, i0p[rb][0] & 0xffff0000u),
+                   __builtin_bit_cast(float, i0p[rb][1] << 16), __builtin_bit_cast(float, i0p[rb][1] & 0xffff0000u)};
+          } else {
+            x = get_own<NP>(ih[l], il[l], rb, g, c);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? dX[rb][r] * elu_d(x[r]) : 0.f;
         }
@@ -857,8 +876,16 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
           if (16 * hb + 4 * g < DTH) {
-            f4* dp = reinterpret_cast<f4*>(&dthl[w][bl][16 * hb + 4 * g]);
-            *dp = *dp + dth4[hb];
+            if constexpr (VISSM_BWD_DTHATOM) {
+              // no-return LDS adds: nothing waits on them (one lane per address: a fixed order)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                __hip_atomic_fetch_add(&dthl[w][bl][16 * hb + 4 * g + r], dth4[hb][r], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              f4* dp = reinterpret_cast<f4*>(&dthl[w][bl][16 * hb + 4 * g]);
+              *dp = *dp + dth4[hb];
+            }
           }
         }
       }
