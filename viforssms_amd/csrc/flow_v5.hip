@@ -349,6 +349,11 @@ __device__ __forceinline__ void fence_fwd() {
 #ifndef VISSM_BWD_DTHATOM
 #define VISSM_BWD_DTHATOM 0  // the per-sample d theta sums as no-return LDS adds
 #endif
+#ifndef VISSM_BWD_BATCHW
+#define VISSM_BWD_BATCHW 6  // bits: 2 the dX fragments read before the head backward, 4 the dcon
+                            // fragments before elu'(I_0) (one hidden layer; reading the recompute's
+                            // fragments a phase ahead as well measured no gain)
+#endif
 #ifndef VISSM_BWD_UNCOND
 #define VISSM_BWD_UNCOND 0
 #endif
@@ -771,6 +776,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // dZ_{NH-1} = (w~_mu gmu + w~_r gr) * elu'(I_NH) -> image NH: the rank-2 outer product is
       // one K = 16 MFMA per row block, A[h][o] = W~h[16 rb + h][o], B[o][p] = (gmu, gr)[o] at p = c
       // (only k-group g = 0 carries the two nonzero k rows)
+      // (VISSM_BWD_BATCHW, one hidden layer: the dX fragments read before the head-backward VALU)
+      Fr8<NP> wb[8];
+      if constexpr ((VISSM_BWD_BATCHW & 2) && NH == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wb[i] = wfrag(sh, 8 * NH + i, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       f4 D[4];
       {
         const bool g0 = g == 0;
@@ -792,6 +804,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
       }
       put_image<NP>(ih[NH], il[NH], D, g, c);
+      Fr8<NP> wcp[2 * JB];  // (VISSM_BWD_BATCHW & 4: the dcon fragments, read before elu'(I_0))
       // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
 #pragma unroll
       for (int l = NH - 1; l >= 0; --l) {
@@ -803,7 +816,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         for (int ks = 0; ks < 2; ++ks) {
           const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
-          for (int ib = 0; ib < 4; ++ib) dX[ib] = mm<NP>(wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane), df, dX[ib]);
+          for (int ib = 0; ib < 4; ++ib)
+            dX[ib] = mm<NP>(((VISSM_BWD_BATCHW & 2) && NH == 1) ? wb[ib * 2 + ks] : wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane),
+                            df, dX[ib]);
         }
         fence_bwd<3>();
 #pragma unroll
@@ -820,6 +835,11 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           if (!(kAbl & 1))
 #pragma unroll
             for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], gb, dWh[hb]);
+        }
+        if constexpr ((VISSM_BWD_BATCHW & 4) && NH == 1) {
+#pragma unroll
+          for (int i = 0; i < 2 * JB; ++i) wcp[i] = wfrag(sh, fwc + i, lane);
+          __builtin_amdgcn_sched_barrier(0);
         }
         // D <- dZ_{l-1} (or dA0 for l = 0) from I_l (read back from its image; row 63 held 1
         // where dI is 0)
@@ -846,7 +866,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       for (int ks = 0; ks < 2; ++ks) {
         const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) dcn[jb] = mm<NP>(wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
+        for (int jb = 0; jb < JB; ++jb)
+          dcn[jb] = mm<NP>(((VISSM_BWD_BATCHW & 4) && NH == 1) ? wcp[jb * 2 + ks] : wfrag(sh, fwc + jb * 2 + ks, lane), df,
+                           dcn[jb]);
         if constexpr (!VISSM_BWD_VALU_DC) {
 #pragma unroll
           for (int o2 = 0; o2 < 2 * !(kAbl & 16); ++o2)
