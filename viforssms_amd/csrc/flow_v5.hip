@@ -350,9 +350,11 @@ __device__ __forceinline__ void fence_fwd() {
 #define VISSM_BWD_DTHATOM 0  // the per-sample d theta sums as no-return LDS adds
 #endif
 #ifndef VISSM_BWD_BATCHW
-#define VISSM_BWD_BATCHW 6  // bits: 2 the dX fragments read before the head backward, 4 the dcon
-                            // fragments before elu'(I_0) (one hidden layer; reading the recompute's
-                            // fragments a phase ahead as well measured no gain)
+#define VISSM_BWD_BATCHW 30  // bits (one hidden layer), all read before the head-backward VALU
+                             // unless noted: 2 the dX weight fragments, 4 the dcon fragments (before
+                             // elu'(I_0)), 8 dW's I_0 fragments, 16 dW_eps's u fragments, 32 the
+                             // transposed conv's carry-in (measured: no further gain, off); reading
+                             // the recompute's fragments a phase ahead measured no gain
 #endif
 #ifndef VISSM_BWD_UNCOND
 #define VISSM_BWD_UNCOND 0
@@ -778,9 +780,21 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       // (only k-group g = 0 carries the two nonzero k rows)
       // (VISSM_BWD_BATCHW, one hidden layer: the dX fragments read before the head-backward VALU)
       Fr8<NP> wb[8];
+      Fr4<NP> xa0[4];  // (VISSM_BWD_BATCHW & 8: dW's I_0 fragments read here as well)
+      Fr4<NP> uaf[JB];  // (& 16: dW_eps's u fragments)
+      float cin_early = 0.f;  // (& 32: the transposed conv's carry-in)
       if constexpr ((VISSM_BWD_BATCHW & 2) && NH == 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) wb[i] = wfrag(sh, 8 * NH + i, lane);
+        if constexpr (VISSM_BWD_BATCHW & 8) {
+#pragma unroll
+          for (int ib = 0; ib < 4; ++ib) xa0[ib] = tr_frag<NP>(ih[0], il[0], ib, g, c);
+        }
+        if constexpr (VISSM_BWD_BATCHW & 16) {
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb) uaf[jb] = ua_frag<NP>(uw, a.s, jb, g, c);
+        }
+        if constexpr (VISSM_BWD_BATCHW & 32) cin_early = mycarry[bl * KP + (lane < a.k ? lane : 0)];
         __builtin_amdgcn_sched_barrier(0);
       }
       f4 D[4];
@@ -823,7 +837,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         fence_bwd<3>();
 #pragma unroll
         for (int ib = 0; ib < 4 * !(kAbl & 2); ++ib) {
-          const Fr4<NP> xa = tr_frag<NP>(ih[l], il[l], ib, g, c);
+          const Fr4<NP> xa = ((VISSM_BWD_BATCHW & 10) == 10 && NH == 1) ? xa0[ib] : tr_frag<NP>(ih[l], il[l], ib, g, c);
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob)
             dW[l][ib][ob] = mm<NP>(xa, tr_frag<NP>(ih[l + 1], il[l + 1], ob, g, c), dW[l][ib][ob]);
@@ -892,7 +906,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const Fr4<NP> ta = tr_frag<NP>(ih[1], il[1], hb, g, c);
         dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mm<NP>(ua_frag<NP>(uw, a.s, jb, g, c), ta, dWe[jb][hb]);
+        for (int jb = 0; jb < JB; ++jb)
+          dWe[jb][hb] = mm<NP>(((VISSM_BWD_BATCHW & 18) == 18 && NH == 1) ? uaf[jb] : ua_frag<NP>(uw, a.s, jb, g, c), ta,
+                               dWe[jb][hb]);
       }
       if (VISSM_BWD_UNCOND || c == 0) {  // (every column of dth4 holds the same sums)
 #pragma unroll
@@ -954,7 +970,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
             if (a.s == 1) v += gw[oq2] * gsc[w][0][oq2];
             else v += (oq2 & 1) ? gw[oq2] * gsc[w][0][oq2 >> 1] : gsc[w][2][oq2 >> 1];
           }
-          const float cin = mycarry[bl * KP + (q < a.k ? q : 0)];
+          const float cin = ((VISSM_BWD_BATCHW & 34) == 34 && NH == 1 && PADDED) ? cin_early
+                                                                                   : mycarry[bl * KP + (q < a.k ? q : 0)];
           if (q < a.k) v += cin;
           if (q < fin) db[t0 + q] = v;
           else if (q < fin + a.k) mycarry[bl * KP + q - fin] = v;

@@ -24,6 +24,20 @@ void set_error(const char* fmt, ...) {
 // (column group, row + offset) so the stream is independent of the launch
 // geometry and of how rows are sharded across ranks.
 // ---------------------------------------------------------------------------
+// Box-Muller on the hardware transcendentals: r = sqrt(-2 ln u1) from v_log_f32 (log2) and
+// v_sqrt_f32, the angle 2 pi u2 through v_sin_f32 / v_cos_f32, whose argument is in revolutions
+// (u2 itself, in (0, 1]) -- no range reduction.  Every kernel that draws the stream uses this.
+__device__ __forceinline__ void box_muller4(u4 r, float (&v)[4]) {
+  constexpr float kM2Ln2 = -1.3862943611198906f;  // -2 ln 2
+  const float r1 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
+  const float r2 = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
+  const float t1 = u01(r.y), t2 = u01(r.w);
+  v[0] = r1 * __builtin_amdgcn_cosf(t1);
+  v[1] = r1 * __builtin_amdgcn_sinf(t1);
+  v[2] = r2 * __builtin_amdgcn_cosf(t2);
+  v[3] = r2 * __builtin_amdgcn_sinf(t2);
+}
+
 // (offset_dev: the row offset read from device memory instead, so a captured graph can advance it)
 __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_t offset,
                                                           const uint64_t* __restrict__ offset_dev,
@@ -38,9 +52,8 @@ __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_
   for (int g = threadIdx.x; g * 4 < L; g += blockDim.x) {
     u4 c{static_cast<uint32_t>(g), 0u, static_cast<uint32_t>(row), static_cast<uint32_t>(row >> 32)};
     u4 r = philox4x32_10(c, k0, k1);
-    float r1 = sqrtf(-2.f * logf(u01(r.x))), r2 = sqrtf(-2.f * logf(u01(r.z)));
-    float a1 = 6.283185307179586f * u01(r.y), a2 = 6.283185307179586f * u01(r.w);
-    float v[4] = {r1 * cosf(a1), r1 * sinf(a1), r2 * cosf(a2), r2 * sinf(a2)};
+    float v[4];
+    box_muller4(r, v);
     const int j0 = g * 4;
     if (j0 + 3 < L) {
       // one 16-byte store (rows are only dword-aligned: L is odd in general)
@@ -75,9 +88,8 @@ __global__ __launch_bounds__(256) void normal_base_short_kernel(uint64_t seed, u
   for (int g = 0; g * 4 < L; ++g) {
     u4 c{static_cast<uint32_t>(g), 0u, static_cast<uint32_t>(row), static_cast<uint32_t>(row >> 32)};
     u4 r = philox4x32_10(c, k0, k1);
-    float r1 = sqrtf(-2.f * logf(u01(r.x))), r2 = sqrtf(-2.f * logf(u01(r.z)));
-    float a1 = 6.283185307179586f * u01(r.y), a2 = 6.283185307179586f * u01(r.w);
-    float v[4] = {r1 * cosf(a1), r1 * sinf(a1), r2 * cosf(a2), r2 * sinf(a2)};
+    float v[4];
+    box_muller4(r, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int j = g * 4 + q;
