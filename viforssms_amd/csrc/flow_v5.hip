@@ -356,6 +356,9 @@ __device__ __forceinline__ void fence_fwd() {
                              // transposed conv's carry-in (measured: no further gain, off); reading
                              // the recompute's fragments a phase ahead measured no gain
 #endif
+#ifndef VISSM_ACC_INIT
+#define VISSM_ACC_INIT 1  // layer-0 products accumulate onto C + theta
+#endif
 #ifndef VISSM_BWD_UNCOND
 #define VISSM_BWD_UNCOND 0
 #endif
@@ -524,9 +527,10 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
     if constexpr (REGW) return wr->f[i];
     else return wfrag(sh, f, lane);
   };
+  // layer 0: the MFMA accumulates onto C + theta (its C operand), so no separate add
   f4 acc[4];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int ob = 0; ob < 4; ++ob) acc[ob] = VISSM_ACC_INIT ? X[ob] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     const Fr8<NP> uf = u_frag<NP>(uw, a.s, kb, g, c);
@@ -536,7 +540,8 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(acc[rb][r] + X[rb][r]) : 0.f;
+    for (int r = 0; r < 4; ++r)
+      X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(VISSM_ACC_INIT ? acc[rb][r] : acc[rb][r] + X[rb][r]) : 0.f;
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     fence_uf<IMG, 6>();
