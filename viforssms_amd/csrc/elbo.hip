@@ -228,19 +228,24 @@ __global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __re
 // IEEE divisions, and the constant terms of the log-densities are added once per sample:
 //   sde = -1/2 sum_t z_t^2 + M (-th2 - log(2 pi)/2),  z_t = (x_{t+1} - th1 x_t - th0) e^{-th2}
 //   obs = -1/2 sum_t bin_t zo_t^2 + (sum_t bin_t)(-log sd - log(2 pi)/2),  zo_t = (x_{t+1} - y_t)/sd
-// (AR.py:169-176).  Per-thread partials are fp32 over at most a few chunks, summed in double in
-// a fixed order.
+// (AR.py:169-176).  One wave per trajectory (kArW per block): the per-sample sums are wave
+// reductions in double (fixed order, no block barrier), and each lane keeps kArU chunks of
+// loads in flight.  Per-lane partials are fp32 over at most a few dozen chunks.
 // ---------------------------------------------------------------------------
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-constexpr int kArV = 4;
+constexpr int kArV = 4;  // consecutive times per chunk (one 16-byte load)
+constexpr int kArU = 4;  // chunks per lane in flight
+constexpr int kArW = 4;  // trajectories (waves) per 256-thread block
 
 __device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 
 __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* __restrict__ z,
                                                           const float* __restrict__ theta, float* __restrict__ sde,
                                                           float* __restrict__ obs) {
-  __shared__ double red[4];
-  const int b = blockIdx.x, M = a.M;
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kArW + (threadIdx.x >> 6));
+  if (b >= a.B) return;  // wave-uniform
+  const int M = a.M;
   const int w = a.d.win ? a.d.win[b] : 0;
   const float* zb = z + static_cast<size_t>(b) * (M + 1);
   const float* yb = a.d.obs + static_cast<size_t>(w) * M;
@@ -248,13 +253,7 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
   const float th0 = theta[b * 3 + 0], th1 = theta[b * 3 + 1], th2 = theta[b * 3 + 2];
   const float is = __expf(-th2), io = 1.f / a.obs_std;
   float sq = 0.f, so = 0.f, sb = 0.f;
-  // transitions t -> t+1, t in [0, M): full chunks of V, then the tail
-  const int nfull = M / kArV;
-  for (int i = threadIdx.x; i < nfull; i += blockDim.x) {
-    const int t0 = kArV * i;
-    const f4u x = ld4(zb + t0);
-    const float xn = zb[t0 + kArV];
-    const f4u y = ld4(yb + t0), bn = ld4(bb + t0);
+  auto chunk = [&](const f4u& x, float xn, const f4u& y, const f4u& bn) {
     const float xs[kArV + 1] = {x[0], x[1], x[2], x[3], xn};
 #pragma unroll
     for (int j = 0; j < kArV; ++j) {
@@ -264,18 +263,39 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
       so += bn[j] * zo * zo;
       sb += bn[j];
     }
+  };
+  // transitions t -> t+1, t in [0, M): full chunks of V (kArU per lane at a time), then the tail
+  const int nfull = M / kArV;
+  int i = lane;
+  for (; i + 64 * (kArU - 1) < nfull; i += 64 * kArU) {
+    f4u x[kArU], y[kArU], bn[kArU];
+    float xn[kArU];
+#pragma unroll
+    for (int q = 0; q < kArU; ++q) {
+      const int t0 = kArV * (i + 64 * q);
+      x[q] = ld4(zb + t0);
+      xn[q] = zb[t0 + kArV];
+      y[q] = ld4(yb + t0);
+      bn[q] = ld4(bb + t0);
+    }
+#pragma unroll
+    for (int q = 0; q < kArU; ++q) chunk(x[q], xn[q], y[q], bn[q]);
   }
-  for (int t = kArV * nfull + threadIdx.x; t < M; t += blockDim.x) {
+  for (; i < nfull; i += 64) {
+    const int t0 = kArV * i;
+    chunk(ld4(zb + t0), zb[t0 + kArV], ld4(yb + t0), ld4(bb + t0));
+  }
+  for (int t = kArV * nfull + lane; t < M; t += 64) {
     const float zt = (zb[t + 1] - th1 * zb[t] - th0) * is;
     const float zo = (zb[t + 1] - yb[t]) * io;
     sq += zt * zt;
     so += bb[t] * zo * zo;
     sb += bb[t];
   }
-  const double rq = block_sum(static_cast<double>(sq), red);
-  const double ro = block_sum(static_cast<double>(so), red);
-  const double rb = block_sum(static_cast<double>(sb), red);
-  if (threadIdx.x == 0) {
+  const double rq = wave_sum(static_cast<double>(sq));
+  const double ro = wave_sum(static_cast<double>(so));
+  const double rb = wave_sum(static_cast<double>(sb));
+  if (lane == 0) {
     sde[b] = static_cast<float>(-0.5 * rq + M * (-static_cast<double>(th2) - 0.5 * kLog2Pi));
     if (obs) obs[b] = static_cast<float>(-0.5 * ro + rb * (-std::log(static_cast<double>(a.obs_std)) - 0.5 * kLog2Pi));
   }
@@ -289,8 +309,10 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
                                                           const float* __restrict__ g_sde,
                                                           const float* __restrict__ g_obs, float* __restrict__ dz,
                                                           float* __restrict__ dtheta) {
-  __shared__ double red[4];
-  const int b = blockIdx.x, M = a.M;
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kArW + (threadIdx.x >> 6));
+  if (b >= a.B) return;  // wave-uniform
+  const int M = a.M;
   const int w = a.d.win ? a.d.win[b] : 0;
   const float* zb = z + static_cast<size_t>(b) * (M + 1);
   float* dzb = dz + static_cast<size_t>(b) * (M + 1);
@@ -318,11 +340,8 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
     return gx;
   };
   // interior chunks: t0 >= 1 and t0 + V <= M, so x_{t0-1} .. x_{t0+V} and obs[t0-1 .. t0+V-2] exist
-  const int ilo = 1, ihi = M / kArV;  // chunks i in [ilo, ihi)
-  for (int i = ilo + threadIdx.x; i < ihi; i += blockDim.x) {
-    const int t0 = kArV * i;
-    const f4u x = ld4(zb + t0), y = ld4(yb + t0 - 1), bn = ld4(bb + t0 - 1);
-    const float xs[kArV + 2] = {zb[t0 - 1], x[0], x[1], x[2], x[3], zb[t0 + kArV]};
+  auto chunk = [&](int t0, const f4u& x, float xp, float xn, const f4u& y, const f4u& bn) {
+    const float xs[kArV + 2] = {xp, x[0], x[1], x[2], x[3], xn};
     f4u g;
 #pragma unroll
     for (int j = 0; j < kArV; ++j) {
@@ -335,10 +354,31 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
       a2 += zt * zt - 1.f;
     }
     *reinterpret_cast<f4u*>(dzb + t0) = g;
+  };
+  const int ilo = 1, ihi = M / kArV;  // chunks i in [ilo, ihi), kArU per lane at a time
+  int i = ilo + lane;
+  for (; i + 64 * (kArU - 1) < ihi; i += 64 * kArU) {
+    f4u x[kArU], y[kArU], bn[kArU];
+    float xp[kArU], xn[kArU];
+#pragma unroll
+    for (int q = 0; q < kArU; ++q) {
+      const int t0 = kArV * (i + 64 * q);
+      x[q] = ld4(zb + t0);
+      xp[q] = zb[t0 - 1];
+      xn[q] = zb[t0 + kArV];
+      y[q] = ld4(yb + t0 - 1);
+      bn[q] = ld4(bb + t0 - 1);
+    }
+#pragma unroll
+    for (int q = 0; q < kArU; ++q) chunk(kArV * (i + 64 * q), x[q], xp[q], xn[q], y[q], bn[q]);
+  }
+  for (; i < ihi; i += 64) {
+    const int t0 = kArV * i;
+    chunk(t0, ld4(zb + t0), zb[t0 - 1], zb[t0 + kArV], ld4(yb + t0 - 1), ld4(bb + t0 - 1));
   }
   // the rest: t in [0, V) and [V ihi, M]
   const int nrest = kArV + (M + 1 - kArV * ihi);
-  for (int r = threadIdx.x; r < nrest; r += blockDim.x) {
+  for (int r = lane; r < nrest; r += 64) {
     const int t = r < kArV ? r : kArV * ihi + (r - kArV);
     if (t > M || (r >= kArV && t < kArV)) continue;  // (M < V: the two ranges overlap)
     const float xc = zb[t];
@@ -347,10 +387,10 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
     dzb[t] = elem(t, xp, xc, xn, y, bn);
   }
   // dlp/dth0 = sum z/s, dlp/dth1 = sum z x_t / s, dlp/dth2 = sum (z^2 - 1)
-  const double r0 = block_sum(static_cast<double>(a0), red);
-  const double r1 = block_sum(static_cast<double>(a1), red);
-  const double r2 = block_sum(static_cast<double>(a2), red);
-  if (threadIdx.x == 0) {
+  const double r0 = wave_sum(static_cast<double>(a0));
+  const double r1 = wave_sum(static_cast<double>(a1));
+  const double r2 = wave_sum(static_cast<double>(a2));
+  if (lane == 0) {
     dtheta[b * 3 + 0] = static_cast<float>(gs * is * r0);
     dtheta[b * 3 + 1] = static_cast<float>(gs * is * r1);
     dtheta[b * 3 + 2] = static_cast<float>(gs * r2);
@@ -412,7 +452,7 @@ int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   dim3 grid(d->B), blk(256);
   prof_begin(VISSM_PROF_ELBO_FWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_fwd_kernel, grid, blk, 0, st, a, z, theta, sde, obs); break;
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_fwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, sde, obs); break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     default: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
@@ -436,7 +476,7 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   dim3 grid(d->B), blk(256);
   prof_begin(VISSM_PROF_ELBO_BWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel, grid, blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     default: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;

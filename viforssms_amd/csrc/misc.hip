@@ -38,18 +38,22 @@ __device__ __forceinline__ void box_muller4(u4 r, float (&v)[4]) {
   v[3] = r2 * __builtin_amdgcn_sinf(t2);
 }
 
+// One wave per row (kNbW rows per 256-thread block): the base log-prob is a wave reduction, no
+// block barrier.
 // (offset_dev: the row offset read from device memory instead, so a captured graph can advance it)
+constexpr int kNbW = 4;
 __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_t offset,
                                                           const uint64_t* __restrict__ offset_dev,
                                                           float* __restrict__ eps, float* __restrict__ base_lp,
-                                                          int L, int n_last) {
-  __shared__ double red[4];
-  const int b = blockIdx.x;
+                                                          int B, int L, int n_last) {
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kNbW + (threadIdx.x >> 6));
+  if (b >= B) return;  // wave-uniform
   const uint64_t row = (offset_dev ? *offset_dev : offset) + static_cast<uint64_t>(b);
   const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
   float* out = eps + static_cast<size_t>(b) * L;
   double acc = 0.0;
-  for (int g = threadIdx.x; g * 4 < L; g += blockDim.x) {
+  for (int g = lane; g * 4 < L; g += 64) {
     u4 c{static_cast<uint32_t>(g), 0u, static_cast<uint32_t>(row), static_cast<uint32_t>(row >> 32)};
     u4 r = philox4x32_10(c, k0, k1);
     float v[4];
@@ -68,8 +72,8 @@ __global__ __launch_bounds__(256) void normal_base_kernel(uint64_t seed, uint64_
     for (int q = 0; q < 4; ++q)
       if (j0 + q < L && j0 + q >= L - n_last) acc += -0.5 * static_cast<double>(v[q]) * v[q];
   }
-  double s = block_sum(acc, red);
-  if (threadIdx.x == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
+  const double s = wave_sum(acc);
+  if (lane == 0) base_lp[b] = static_cast<float>(s - 0.5 * kLog2Pi * n_last);
 }
 
 // Short rows (the q(theta) base draws, L = P_theta): one thread per row, the same Philox stream
@@ -108,7 +112,8 @@ static void launch_normal(uint64_t seed, uint64_t offset, const uint64_t* offset
     hipLaunchKernelGGL(normal_base_short_kernel, dim3((B + 255) / 256), dim3(256), 0, st, seed, offset, offset_dev, eps,
                        base_lp, B, L, n_last);
   else
-    hipLaunchKernelGGL(normal_base_kernel, dim3(B), dim3(256), 0, st, seed, offset, offset_dev, eps, base_lp, L, n_last);
+    hipLaunchKernelGGL(normal_base_kernel, dim3((B + kNbW - 1) / kNbW), dim3(256), 0, st, seed, offset, offset_dev, eps,
+                       base_lp, B, L, n_last);
 }
 
 __global__ __launch_bounds__(256) void base_logprob_kernel(const float* __restrict__ eps, float* __restrict__ base_lp,
