@@ -205,7 +205,15 @@ constexpr int kAbl = VISSM_V5_ABLATE;
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
+  int dcb;  // backward: the block's waves share a chunk and sum their dC tiles (one window)
 };
+
+// backward dC tiles summed over a block's NW groups before the slab (one window only): the dC
+// slab per AR-cfg launch 4.1 -> 1.0 GB and its reduce 0.74 -> 0.19 ms, but the tile barriers'
+// wave skew costs the kernel 0.8 ms: measured 126.9 vs 125.8 ms per AR-cfg step, so off
+#ifndef VISSM_BWD_DCB
+#define VISSM_BWD_DCB 0
+#endif
 
 // folded hidden weight W~_l[hin][hout] and head weight W~_h[h][o]
 __device__ __forceinline__ float wt_hid(const VissmFlowParams& w, int H, int bn, int l, int hin, int hout) {
@@ -687,11 +695,27 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int i = threadIdx.x; i < NW * KP * QW; i += NT) (&dscr[0][0][0])[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
-  if (item >= a.n_items) return;  // no block-level synchronisation below this point
-  const int grp = item / a.n_chunks, chn = item % a.n_chunks;
+  // Work items (sample group x t-chunk), one per wave.  With a.dcb (one window) the block's NW
+  // waves take NW consecutive groups of the SAME chunk and sum their dC tiles through LDS at each
+  // tile's end (fixed order), so the dC slab holds one row per block of groups; otherwise a
+  // block's waves are independent and no block-level synchronisation follows.
+  int item, grp, chn;
+  if (a.dcb) {
+    chn = blockIdx.x % a.n_chunks;
+    grp = (blockIdx.x / a.n_chunks) * NW + w;
+    item = grp * a.n_chunks + chn;
+  } else {
+    item = blockIdx.x * NW + w;
+    grp = item / a.n_chunks;
+    chn = item % a.n_chunks;
+  }
+  item = __builtin_amdgcn_readfirstlane(item);  // wave-uniform: scalar loads of per-sample data
+  grp = __builtin_amdgcn_readfirstlane(grp);
+  chn = __builtin_amdgcn_readfirstlane(chn);
+  const bool valid = grp < a.n_groups;
+  if (!a.dcb && !valid) return;  // (dcb: an idle wave still joins the block's tile barriers)
   const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
-  const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
+  const int b_lo = grp * a.S, nb = valid ? min(a.S, a.B - b_lo) : 0;
   __bf16* ih[NS];
   __bf16* il[NS];
 #pragma unroll
@@ -983,8 +1007,26 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
       }
     }
-    // tile done: its dC over the group
-    if (c < nP) {
+    // tile done: its dC over the group (dcb: over the block's groups, summed through the waves'
+    // image slots -- free until the next unit -- in wave order)
+    if (a.dcb) {
+      float* mine = reinterpret_cast<float*>(&timg[w][0][0][0]);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * rb + r < NR) mine[(4 * rb + r) * 64 + lane] = dCa[rb][r];
+      __syncthreads();
+      float* dcs = dC_slab + (static_cast<size_t>(blockIdx.x / a.n_chunks) * a.Lh + m0) * a.H;
+      for (int i = w; i < NR; i += NW) {  // register row i of every lane
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += reinterpret_cast<const float*>(&timg[v][0][0][0])[i * 64 + lane];
+        const int h = swz(16 * (i >> 2) + 4 * g + (i & 3));
+        if (c < nP && h < a.H) dcs[c * a.H + h] = s * kLog2e;
+      }
+      __syncthreads();
+    } else if (c < nP) {
       float* dcs = dC_slab + (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
@@ -996,6 +1038,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     }
   }
 
+  if (!valid) return;
   // ---- per-sample tails: carry -> halo / du tail; d theta -> slab ----
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
@@ -1056,6 +1099,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 struct Geom {
   int s, Lout, Lh, S, n_groups, n_tiles, CH, n_chunks, n_items;
+  int dcb, n_dc;  // block-summed dC tiles (backward, one window); dC slab rows
+  int blocks;     // grid size
 };
 
 static Geom geom(const VissmFlowDesc* d, bool backward) {
@@ -1079,6 +1124,9 @@ static Geom geom(const VissmFlowDesc* d, bool backward) {
   g.CH = tiles_per_chunk * P;
   g.n_chunks = (g.Lh + g.CH - 1) / g.CH;
   g.n_items = g.n_groups * g.n_chunks;
+  g.dcb = (backward && d->n_win == 1 && VISSM_BWD_DCB) ? 1 : 0;
+  g.n_dc = g.dcb ? (g.n_groups + NW - 1) / NW : g.n_groups;
+  g.blocks = g.dcb ? g.n_dc * g.n_chunks : (g.n_items + NW - 1) / NW;
   return g;
 }
 
@@ -1111,7 +1159,7 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   if (!backward) {
     t.ls_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * 4));
   } else {
-    t.dC_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_groups) * g.Lh * d->H * 4));
+    t.dC_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_dc) * g.Lh * d->H * 4));
     t.dth_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * d->H * 4));
     t.dW_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_items) * n_wgrad(d) * 4));
     t.halo = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * g.n_chunks * d->k * 4));
@@ -1126,6 +1174,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
+  a.dcb = g.dcb;
   return a;
 }
 
@@ -1287,7 +1336,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
-  dim3 grid((g.n_items + NW - 1) / NW);
+  dim3 grid(g.blocks);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   FLOW5_DISPATCH(bwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next,
                  dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
@@ -1301,7 +1350,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   int rc;
   if (d->n_win == 1) {
-    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_groups, nC, st);
+    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
     if (rc) return rc;
   } else {
     dim3 rg(static_cast<unsigned>((nC + 255) / 256), d->n_win);
