@@ -234,10 +234,20 @@ __global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __re
 // ---------------------------------------------------------------------------
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 constexpr int kArV = 4;  // consecutive times per chunk (one 16-byte load)
-constexpr int kArU = 4;  // chunks per lane in flight
-constexpr int kArW = 4;  // trajectories (waves) per 256-thread block
+#ifndef VISSM_AR_U
+#define VISSM_AR_U 8
+#endif
+#ifndef VISSM_AR_NT
+#define VISSM_AR_NT 0  // z read with non-temporal loads (read once)
+#endif
+constexpr int kArU = VISSM_AR_U;  // chunks per lane in flight
+constexpr int kArW = 4;           // trajectories (waves) per 256-thread block
 
 __device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
+__device__ __forceinline__ f4u ldz4(const float* p) {
+  if constexpr (VISSM_AR_NT) return __builtin_nontemporal_load(reinterpret_cast<const f4u*>(p));
+  return ld4(p);
+}
 
 __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* __restrict__ z,
                                                           const float* __restrict__ theta, float* __restrict__ sde,
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
 #pragma unroll
     for (int q = 0; q < kArU; ++q) {
       const int t0 = kArV * (i + 64 * q);
-      x[q] = ld4(zb + t0);
+      x[q] = ldz4(zb + t0);
       xn[q] = zb[t0 + kArV];
       y[q] = ld4(yb + t0);
       bn[q] = ld4(bb + t0);
@@ -283,7 +293,7 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
   }
   for (; i < nfull; i += 64) {
     const int t0 = kArV * i;
-    chunk(ld4(zb + t0), zb[t0 + kArV], ld4(yb + t0), ld4(bb + t0));
+    chunk(ldz4(zb + t0), zb[t0 + kArV], ld4(yb + t0), ld4(bb + t0));
   }
   for (int t = kArV * nfull + lane; t < M; t += 64) {
     const float zt = (zb[t + 1] - th1 * zb[t] - th0) * is;
@@ -363,7 +373,7 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
 #pragma unroll
     for (int q = 0; q < kArU; ++q) {
       const int t0 = kArV * (i + 64 * q);
-      x[q] = ld4(zb + t0);
+      x[q] = ldz4(zb + t0);
       xp[q] = zb[t0 - 1];
       xn[q] = zb[t0 + kArV];
       y[q] = ld4(yb + t0 - 1);
@@ -374,7 +384,7 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
   }
   for (; i < ihi; i += 64) {
     const int t0 = kArV * i;
-    chunk(t0, ld4(zb + t0), zb[t0 - 1], zb[t0 + kArV], ld4(yb + t0 - 1), ld4(bb + t0 - 1));
+    chunk(t0, ldz4(zb + t0), zb[t0 - 1], zb[t0 + kArV], ld4(yb + t0 - 1), ld4(bb + t0 - 1));
   }
   // the rest: t in [0, V) and [V ihi, M]
   const int nrest = kArV + (M + 1 - kArV * ihi);
