@@ -1,5 +1,6 @@
-// ELBO log-density kernels: one 256-thread block per trajectory, fixed-order
-// block reductions (double accumulation).  Streaming: the path z is read once
+// ELBO log-density kernels: one 256-thread block per trajectory (LV, SV, FHN) or one
+// wave per trajectory (AR, the streaming path below), fixed-order block / wave
+// reductions (double accumulation).  Streaming: the path z is read once
 // (forward) or once plus its neighbours (backward, which recomputes each
 // transition from both of its endpoints instead of exchanging partials).
 //
