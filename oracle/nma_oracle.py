@@ -54,12 +54,17 @@ def dense(x, w, b, act=None):
 
 
 def conv1d_valid(x, w, b, stride=1):
-    """tf.layers.conv1d(padding='valid'): out[t] = sum_j x[s*t + j] . W[j] + b (AR.py:61-62)."""
+    """tf.layers.conv1d(padding='valid'): out[t] = sum_j x[s*t + j] . W[j] + b (AR.py:61-62).
+
+    Evaluated as one [n_out, C] x [C, H] product per tap, so the memory stays O(L C) even for
+    LV's kernel_ext-channel input (lotka_volterra_partial.py:78-79)."""
     k = w.shape[0]
     L = x.shape[1]
     n_out = (L - k) // stride + 1
-    win = x.unfold(1, k, 1)[:, : (n_out - 1) * stride + 1 : stride]  # [p, n_out, C, k]
-    return torch.einsum("ptck,kch->pth", win, w) + b
+    out = b
+    for j in range(k):
+        out = out + x[:, j: j + (n_out - 1) * stride + 1: stride, :] @ w[j]
+    return out
 
 
 # --------------------------------------------------------------------------------------
@@ -166,10 +171,13 @@ def theta_term(theta, P):
     return dense(t, P["th_w2"], P["th_b2"])
 
 
-def iaf_flow(u, F, theta, P, cfg: FlowCfg):
-    """One IAF._create_flow: returns (u_next [p, L-k], sigma_log [p, n_logsig])."""
-    conv_in = torch.cat([u[:, :-1, None], F], dim=2)
-    a = conv1d_valid(conv_in, P["conv_w"], P["conv_b"]) + theta_term(theta, P)[:, None, :]
+def iaf_flow(u, CF, theta, P, cfg: FlowCfg):
+    """One IAF._create_flow: returns (u_next [p, L-k], sigma_log [p, n_logsig]).
+
+    The first conv acts on concat(u[:, :-1], F) (AR.py:58-62); it is linear in its input
+    channels, so it is evaluated as conv(u channel) + CF, CF = conv(F channels) + bias from
+    `window_conv` (computed once per distinct window and gathered per sample)."""
+    a = conv1d_valid(u[:, :-1, None], P["conv_w"][:, :1, :], 0.0) + CF + theta_term(theta, P)[:, None, :]
     h = elu(a)
     for l in range(cfg.n_hidden):
         h = elu(h @ P[f"hid_w{l}"] + P[f"hid_b{l}"])
@@ -188,22 +196,28 @@ def iaf_flow(u, F, theta, P, cfg: FlowCfg):
     return u[:, cfg.k:] * sig + mu, sigma_log
 
 
+def window_conv(F, P):
+    """Feature channels of the first conv plus its bias, for each distinct window: [w, L-k, H]."""
+    return conv1d_valid(F, P["conv_w"][:, 1:, :], P["conv_b"])
+
+
 def swap_pairs(x):
     """Permute between 2-D flows: scatter_nd with perm list [1,0,3,2,...] (lotka_volterra_partial.py:207-213)."""
     p, L = x.shape
     return x.reshape(p, L // 2, 2).flip(-1).reshape(p, L)
 
 
-def flow_stack(eps, feats_per_flow, theta, flows_P, cfg: FlowCfg, permute: bool):
+def flow_stack(eps, conv_feats, theta, flows_P, cfg: FlowCfg, permute: bool):
     """Flow_Stack (AR.py:92-110; LV adds Permute between flows, last one dropped, lotka_volterra_partial.py:277-288).
 
-    feats_per_flow[i] is flow i's window-shared F tensor.  Returns (sample, log q)."""
+    conv_feats[i] is flow i's per-sample feature-channel conv term (window_conv gathered per sample).
+    Returns (sample, log q)."""
     base_lp = normal_logpdf(eps, 0.0, 1.0)[:, -cfg.n_logsig:].sum(1)   # init_dist.slp (AR.py:31-35)
     u = eps
     lq = base_lp
     n = len(flows_P)
     for i in range(n):
-        u, sl = iaf_flow(u, feats_per_flow[i], theta, flows_P[i], cfg)
+        u, sl = iaf_flow(u, conv_feats[i], theta, flows_P[i], cfg)
         lq = lq - sl.sum(1)
         if permute and i < n - 1:
             u = swap_pairs(u)
@@ -436,10 +450,14 @@ def elbo(spec: ModelSpec, params, perms, x0_theta, eps, time_feats, extra):
     theta, logq_theta = qtheta_sample_logprob(x0_theta, spec.base_loc, spec.base_scale,
                                               build_bijectors(params, perms), act)
     cfg = spec.flow_cfg()
+    # the feature branch and the feature channels of the first conv depend on the window only:
+    # evaluate them once per distinct time_feats row and gather per sample
+    uniq, inv = torch.unique(time_feats, dim=0, return_inverse=True)
     feats = []
     for i in range(spec.n_flows):
-        ts = time_feats if spec.family == "lv" else time_feats[:, i * spec.k:, :]
-        feats.append(flow_features(ts, params["flows"][i], cfg))
+        ts = uniq if spec.family == "lv" else uniq[:, i * spec.k:, :]
+        P = params["flows"][i]
+        feats.append(window_conv(flow_features(ts, P, cfg), P)[inv])
     z, lq = flow_stack(eps, feats, theta, params["flows"], cfg, permute=spec.D == 2)
     scale = spec.target / spec.M
     prior = prior_logprob(theta, spec.priors)
@@ -518,3 +536,75 @@ def ar_time_feats(obs, obs_bin, time_till, n_flows, k, M, fw, T, starts):
         for c, arr in enumerate(chans):
             out[r, :, c] = arr[s:s + kext]
     return out
+
+
+def _gather_rows(arr, idx, length):
+    """[len(idx), length] = arr[i : i + length] for each start i (the reference's per-start slices)."""
+    return np.stack([np.asarray(arr[int(i):int(i) + length]) for i in idx])
+
+
+def pair_time_feats(family, obs, obs_bin, time_till, x0, dt, T, target_dims, n_flows, k, M, fw, starts):
+    """LV / FHN host feeds for window starts `starts` (reference batch_select):
+    LV lotka_volterra_partial.py:185-204 (arrays) + :366-386 (per-step gather);
+    FHN fitz_nag_NVP.py:182-202 + :346-366.
+
+    Returns dict(time_feats [p, kext, fw+3], mask [p,2,M+1], shift [p,2,M+1], bin [p,2,M]).
+    The two families differ in bin_feats (LV zeros then ones, FHN ones then zeros) and in the
+    time_till pad arange, which FHN runs down to -dt (one pair longer than the other pads)."""
+    D = 2
+    lead = n_flows * k + D                                 # zeros before the series in every pad
+    kext = n_flows * k + D * M + 2
+    series = np.asarray(obs).T.reshape(-1)                 # np.reshape(obs, -1, 'F'): t-major interleave
+    lag_arrays = []
+    for lag in range(0, 5 * fw, 5):
+        lag_arrays.append(np.concatenate((np.zeros(lead - lag), series, np.zeros(lag))))
+    times = np.concatenate((np.zeros(lead), np.repeat(np.arange(dt, T + dt, dt), D)))
+    stop = 0.0 if family == "lv" else -dt
+    head = np.arange(np.round(lead * (dt / D), 1), stop, -dt)
+    tt_pad = np.repeat(head, D).reshape(-1, D).T          # np.reshape(np.repeat(.), (2, -1), 'F')
+    till = np.concatenate((tt_pad, np.asarray(time_till)), 1).T.reshape(-1)
+    if family == "lv":
+        binf = np.float32(np.concatenate((np.zeros(lead), np.ones(target_dims * D))))
+    else:
+        binf = np.float32(np.concatenate((np.ones(lead), np.zeros(target_dims * D))))
+    mask_vals = np.concatenate((np.zeros((2, 1)), np.ones((D, target_dims))), axis=1)
+    shift_vals = np.concatenate((np.asarray(x0, dtype=np.float64)[:, None], np.zeros((D, target_dims))), axis=1)
+    idx = D * np.asarray(starts, dtype=np.int64)
+    chans = [_gather_rows(a, idx, kext) for a in lag_arrays]
+    chans += [_gather_rows(binf, idx, kext), _gather_rows(times, idx, kext), _gather_rows(till, idx, kext)]
+    ts = np.stack(chans, axis=2).astype(np.float64)
+    st = np.asarray(starts, dtype=np.int64)
+    mask = np.stack([mask_vals[:, s:s + M + 1] for s in st])
+    shift = np.stack([shift_vals[:, s:s + M + 1] for s in st])
+    ob = np.asarray(obs_bin, dtype=np.float64)
+    binfeed = np.stack([ob[:, s:s + M] for s in st])
+    return {"time_feats": ts, "mask": mask, "shift": shift, "bin": binfeed}
+
+
+def sv_time_feats(obs, x0, dt, T, target_dims, n_flows, k, M, fw, starts):
+    """SV host feeds (SV_dense.py:159-185 arrays, :304-328 per-step gather).
+
+    Channels [obs lags 0,5,..,5(fw-1); time; rolling var of obs; log rolling var of the
+    differences], rolling windows of kernel_len on the float32 series as loaded.
+    Returns dict(time_feats [p, kext, fw+3], mask [p, M+1], shift [p, M+1], dim_one [p, M+1])."""
+    obs = np.asarray(obs)
+    n = obs.shape[0]
+    lead = n_flows * k
+    kext = n_flows * k + M + 1
+    rv = np.array([np.var(obs[i:i + k]) for i in range(n - k)])
+    dif = obs[1:] - obs[:-1]
+    rvd = np.array([np.var(dif[i:i + k]) for i in range(dif.shape[0] - k)])
+    var_pad = np.concatenate((np.zeros(lead + k), rv))
+    var_diff_pad = np.concatenate((np.zeros(lead + k), np.log(rvd), np.zeros(1)))
+    lag_arrays = [np.concatenate((np.zeros(lead - lag), obs, np.zeros(lag))) for lag in range(0, 5 * fw, 5)]
+    times = np.concatenate((np.zeros(lead + 1), np.arange(0.1, T + dt, dt)))
+    st = np.asarray(starts, dtype=np.int64)
+    chans = [_gather_rows(a, st, kext) for a in lag_arrays]
+    chans += [_gather_rows(times, st, kext), _gather_rows(var_pad, st, kext), _gather_rows(var_diff_pad, st, kext)]
+    ts = np.stack([c.astype(np.float64) for c in chans], axis=2)
+    mask_vals = np.concatenate((np.zeros(1), np.ones(target_dims)))
+    shift_vals = np.concatenate((np.array([x0], dtype=np.float64), np.zeros(target_dims)))
+    return {"time_feats": ts,
+            "mask": np.stack([mask_vals[s:s + M + 1] for s in st]),
+            "shift": np.stack([shift_vals[s:s + M + 1] for s in st]),
+            "dim_one": np.stack([obs[s:s + M + 1].astype(np.float64) for s in st])}

@@ -13,7 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from tests.parity_util import build_model, oracle_reference  # noqa: E402
 
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle_cases.npz")
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "oracle_cases.npz")
+OUT_CFG = os.path.join(HERE, "oracle_cases_cfg.npz")
 # name: (family, B, M, k, n_flows, H, n_layers, fw, T, starts)
 CASES = {
     "ar_small": ("ar", 5, 24, 4, 2, 16, 3, 3, None, None),
@@ -23,11 +25,18 @@ CASES = {
     "sv_small": ("sv", 4, 24, 6, 2, 16, 5, 3, None, None),
     "fhn_small": ("fhn", 4, 40, 6, 2, 24, 5, 3, 160, [120, 0, 40, 80]),
 }
+# BASELINE configs[1] at its own length (AR(1) T = M = 5000, impute 5, kernel_len 8, 3 flows, [50]*3),
+# conditioned parameter draw (parity_util.build_model(condition=True)); a file of its own (~1 MB)
+CFG_CASES = {
+    "ar_cfg_length": ("ar", 4, 5000, 8, 3, 50, 3, 10, None, None),
+}
+CFG_OPTS = {"ar_cfg_length": dict(impute=5, condition=True)}
 
 
 def case_arrays(name, cfg, seed=3):
     family, B, M, k, nf, H, nl, fw, T, starts = cfg
-    model = build_model(family, B, M, k, nf, H, nl, fw, "cpu", T=T, seed=seed)
+    opts = CFG_OPTS.get(name, {})
+    model = build_model(family, B, M, k, nf, H, nl, fw, "cpu", T=T, seed=seed, **opts)
     md = model.mdef
     starts = np.zeros(B, dtype=np.int64) if starts is None else np.asarray(starts, dtype=np.int64)
     batch = model.engine.make_batch(starts)
@@ -40,19 +49,28 @@ def case_arrays(name, cfg, seed=3):
     st = model.store
     gflat = np.concatenate([np.asarray(grads[n], dtype=np.float64).ravel() for n in st.names()])
     pre = name + "/"
-    return {pre + "cfg": np.array([B, M, k, nf, H, nl, fw, -1 if T is None else T], dtype=np.int64),
+    return {pre + "cfg": np.array([B, M, k, nf, H, nl, fw, -1 if T is None else T, opts.get("impute", 0),
+                                   int(opts.get("condition", False))], dtype=np.int64),
             pre + "family": np.array(family), pre + "starts": starts,
             pre + "flat": st.flat.detach().cpu().numpy().astype(np.float32),
             pre + "eps": eps.numpy().astype(np.float32), pre + "x0": x0.numpy().astype(np.float32),
             pre + "elbo": elbo, pre + "grad": gflat.astype(np.float32)}
 
 
-def main():
+def write(path, cases):
     arrs = {}
-    for name, cfg in CASES.items():
+    for name, cfg in cases.items():
         arrs.update(case_arrays(name, cfg))
-    np.savez_compressed(OUT, names=np.array(list(CASES)), **arrs)
-    print("wrote", OUT, os.path.getsize(OUT), "bytes")
+    np.savez_compressed(path, names=np.array(list(cases)), **arrs)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def main():
+    which = sys.argv[1:] or ["small", "cfg"]
+    if "small" in which:
+        write(OUT, CASES)
+    if "cfg" in which:
+        write(OUT_CFG, CFG_CASES)
 
 
 if __name__ == "__main__":

@@ -105,3 +105,54 @@ def test_sv_table_shapes():
     assert w.shape == (2, 303, 8) and np.all(np.isfinite(w))
     f = tab.feeds([0, 52])
     assert f["dim_one"].shape == (2, 53) and np.allclose(f["dim_one"][1], obs[52:105])
+
+
+# --- LV / FHN / SV host feeds against the oracle's independent restatement (bit-exact) ---------
+@pytest.mark.parametrize("family", ["lv", "fhn"])
+@pytest.mark.parametrize("n,k,M,fw,starts", [(3, 20, 50, 10, [0, 50, 450, 50]), (2, 4, 24, 3, [0, 24, 48, 456]),
+                                              (3, 20, 500, 10, [0])])
+def test_pair_tables_match_oracle_on_reference_files(family, n, k, M, fw, starts):
+    """dat/LV_* through features.lv_table / fhn_table == oracle.pair_time_feats
+    (lotka_volterra_partial.py:185-204, 366-386; fitz_nag_NVP.py:182-202, 346-366)."""
+    obs, ob, tt = data.load_lv()
+    x0 = np.array([100.0, 100.0]) if family == "lv" else np.array([2.0, 3.0])
+    mk = features.lv_table if family == "lv" else features.fhn_table
+    tab = mk(obs, ob, tt, x0, 50.0, 0.1, 500, n, k, M, fw)
+    ref = O.pair_time_feats(family, obs, ob, tt, x0, 0.1, 50.0, 500, n, k, M, fw, starts)
+    assert np.array_equal(tab.windows(starts), ref["time_feats"])
+    f = tab.feeds(starts)
+    assert np.array_equal(f["obs_bin"], ref["bin"])
+    if family == "lv":
+        assert np.array_equal(f["mask"], ref["mask"]) and np.array_equal(f["shift"], ref["shift"])
+
+
+@pytest.mark.parametrize("family,T,k,starts", [("lv", 5000, 20, [0]), ("fhn", 2000, 20, [0]),
+                                               ("lv", 1000, 20, [0, 500, 500])])
+def test_pair_tables_match_oracle_at_config_lengths(family, T, k, starts):
+    """The BASELINE configs' lengths (LV T = 5000, FHN T = 2000) on simulated series."""
+    gen = data.lv_data_gen if family == "lv" else data.fhn_data_gen
+    obs, ob, tt, _ = gen(T, dt=0.1, obs_every=100 if family == "lv" else 10, seed=1)
+    x0 = np.array([100.0, 100.0]) if family == "lv" else np.array([2.0, 3.0])
+    M = T // max(1, len(set(starts)))
+    mk = features.lv_table if family == "lv" else features.fhn_table
+    tab = mk(obs, ob, tt, x0, T * 0.1, 0.1, T, 3, k, M, 10)
+    ref = O.pair_time_feats(family, obs, ob, tt, x0, 0.1, T * 0.1, T, 3, k, M, 10, starts)
+    assert np.array_equal(tab.windows(starts), ref["time_feats"])
+    f = tab.feeds(starts)
+    assert np.array_equal(f["obs_bin"], ref["bin"])
+    if family == "lv":
+        assert np.array_equal(f["mask"], ref["mask"]) and np.array_equal(f["shift"], ref["shift"])
+
+
+@pytest.mark.parametrize("n,k,M,fw,starts", [(5, 50, 52, 5, [0, 52, 1456, 52]), (5, 50, 1508, 5, [0]),
+                                              (2, 6, 24, 3, [0, 24, 1200])])
+def test_sv_table_matches_oracle(n, k, M, fw, starts):
+    """dat/SV.dat[300:] through features.sv_table == oracle.sv_time_feats (SV_dense.py:159-185, 304-328)."""
+    obs = data.load_sv()
+    T = obs.shape[0] - 1
+    tab = features.sv_table(obs, -8.5, T, 1.0, T, n, k, M, fw)
+    ref = O.sv_time_feats(obs, -8.5, 1.0, T, T, n, k, M, fw, starts)
+    assert np.array_equal(tab.windows(starts), ref["time_feats"])
+    f = tab.feeds(starts)
+    for key in ("mask", "shift", "dim_one"):
+        assert np.array_equal(f[key], ref[key]), key

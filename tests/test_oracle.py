@@ -43,10 +43,22 @@ def test_zero_weight_flow_analytic_logq():
     P["head_b"] = torch.tensor([0.7, -0.3], dtype=DT)
     u = torch.randn(2, 12, dtype=DT)
     F = torch.randn(2, 11, 4, dtype=DT)
-    out, sl = O.iaf_flow(u, F, torch.randn(2, 2, dtype=DT), P, cfg)
+    out, sl = O.iaf_flow(u, O.window_conv(F, P), torch.randn(2, 2, dtype=DT), P, cfg)
     sig = math.log1p(math.exp(-0.3)) + 1e-10
     assert torch.allclose(out, u[:, 3:] * sig + 0.7)
     assert torch.allclose(sl, torch.full((2, 5), math.log(sig), dtype=DT))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv1d_valid_matches_torch_conv(stride):
+    """The per-tap product form of tf.layers.conv1d(padding='valid') equals torch's own conv1d
+    (cross-correlation, channels-last kernel [k, C_in, C_out])."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 41, 7, generator=g, dtype=DT)
+    w = torch.randn(6, 7, 5, generator=g, dtype=DT)
+    b = torch.randn(5, generator=g, dtype=DT)
+    ref = torch.nn.functional.conv1d(x.transpose(1, 2), w.permute(2, 1, 0), b, stride=stride).transpose(1, 2)
+    assert torch.allclose(O.conv1d_valid(x, w, b, stride), ref, rtol=1e-12, atol=1e-12)
 
 
 def test_ar_density_known_points():
