@@ -110,13 +110,6 @@ typedef struct {        /* outputs of the backward: written, not accumulated */
   float* w_head; float* b_head;
 } VissmFlowGrads;
 
-/* Selects the fp32 flow implementation for A/B measurements (default 0 = by shape:
- * 4 for one hidden layer, 2 otherwise; 4 = matrix cores,
- * latency-hiding [default]; 3 = matrix cores, 8-wave blocks; 2 = matrix cores,
- * 4-wave blocks; 1 = VALU/LDS).
- * 0 only queries.  Returns the previous selection. */
-int vissm_flow_set_impl(int32_t which);
-
 /* C is [n_win][Lh][H] with Lh = (L-k) (stride 1) or (L-k)/2 (stride 2);
  * win is [B] int32 window index per sample (NULL = all 0). */
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward);

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--H", type=int, default=50)
     ap.add_argument("--nh", type=int, default=1)
     ap.add_argument("--stride2", action="store_true")
-    ap.add_argument("--impls", default="2,3")
+    ap.add_argument("--impls", default="fp32,bf16", help="flow precisions to time: fp32, bf16, bf16x3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="", help="run only this impl (for PMC passes)")
     args = ap.parse_args()
@@ -44,8 +44,8 @@ def main():
     w_head, b_head = r(H, 2, sc=0.2), r(2, sc=0.1)
     gnext, gls = r(B, sh.Lout), r(B)
     # entries: an fp32 implementation number (1-4) or "bf16" / "bf16x3" (matrix-core bf16 kernels)
-    PREC = {"bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}
-    impls = [x if x in PREC else int(x) for x in (args.only or args.impls).split(",")]
+    PREC = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}
+    impls = [x if x in PREC else "fp32" for x in (args.only or args.impls).split(",")]  # legacy 2/4 -> fp32
     import dataclasses
     res = {}
     outs = {}
@@ -60,11 +60,7 @@ def main():
         for im in impls:
             lib.vissm_profile_reset()
             lib.vissm_profile_enable(1 if rd > 0 else 0)
-            shp = sh
-            if im in PREC:
-                shp = dataclasses.replace(sh, precision=PREC[im])
-            else:
-                lib.vissm_flow_set_impl(im)
+            shp = dataclasses.replace(sh, precision=PREC[im])
             ins = [t.clone().requires_grad_(True) for t in (u, C, tt, w_eps, w_hid, b_hid, w_head, b_head)]
             extra = [bn_g, bn_b]
             torch.cuda.synchronize()

@@ -71,7 +71,6 @@ SIGNATURES = {
                                  _f32, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
-    "vissm_flow_set_impl": (_i32, [_i32]),
     "vissm_profile_enable": (None, [_i32]),
     "vissm_profile_read": (_i32, [_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "vissm_profile_reset": (None, []),

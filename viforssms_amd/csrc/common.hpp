@@ -111,6 +111,12 @@ int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipS
 // same result, two passes for few columns / many rows; uses the slab's part-head rows as scratch
 int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hipStream_t st);
 
+// flow epilogues shared by the flow implementations (flow_common.hip)
+int launch_halo_fixup(float* du, const float* halo, int B, int L, int k, int n_chunks, int s, int CH, hipStream_t st);
+int launch_reduce_by_window(const float* slab, const int32_t* win, float* out, int B, int n_win, int64_t N,
+                            hipStream_t st);
+int launch_scatter_wgrad(const float* red, const VissmFlowGrads* g, int k, int H, int nh, int bn, hipStream_t st);
+
 // opt-in event timing of main kernels (vissm_profile_*)
 bool prof_on();
 void prof_begin(int kind, hipStream_t st);

@@ -1,29 +1,18 @@
 // C-ABI entry points of the IAF flow (include/vissm.h): argument validation and
-// dispatch to the implementation.  flow4 (matrix cores, exact fp32, latency
-// hiding) is the product path; flow3 (8-wave blocks), flow2 (4-wave blocks)
-// and flow1 (LDS-tiled VALU fp32) are kept as independent implementations for
-// A/B checks, selected with VISSM_FLOW_IMPL / vissm_flow_set_impl().
+// dispatch by precision and shape.  bf16 / bf16x3 run on the bf16 matrix-core kernels
+// (flow_v5) where they cover the shape; fp32 runs the exact-fp32 matrix-core kernels:
+// flow4 (register-resident weights, latency hiding) for one hidden layer, flow2 for
+// deeper heads (LV / SV / FHN), where flow4's register-resident weights do not apply
+// and it measured slower (LV-like shape: 64 vs 76 ms bwd).  No process state.
 #include "common.hpp"
-
-#include <cstdlib>
 
 namespace vissm {
 
-size_t flow1_workspace_size(const VissmFlowDesc* d, int backward);
-int flow1_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
-              float*, float*, void*, size_t, hipStream_t);
-int flow1_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
-              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
-size_t flow3_workspace_size(const VissmFlowDesc* d, int backward);
 size_t flow4_workspace_size(const VissmFlowDesc* d, int backward);
 int flow4_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               float*, float*, void*, size_t, hipStream_t);
 int flow4_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
-              const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
-int flow3_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
-              float*, float*, void*, size_t, hipStream_t);
-int flow3_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 int flow2_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               float*, float*, void*, size_t, hipStream_t);
@@ -37,23 +26,7 @@ int flow5_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 int flow5_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 
-static int g_impl = 0;  // 0 = not chosen yet
-
-static int impl_choice() {
-  if (g_impl == 0) {
-    const char* e = std::getenv("VISSM_FLOW_IMPL");
-    g_impl = (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : -1;  // -1: by shape
-  }
-  return g_impl;
-}
-
-// fp32 path: flow4 for the one-hidden-layer (AR) shapes; flow2 for deeper heads, where flow4's
-// register-resident weights do not apply and it measured slower (LV-like shape: 64 vs 76 ms bwd)
-static int impl_for(const VissmFlowDesc* d) {
-  const int c = impl_choice();
-  if (c > 0) return c;
-  return d->n_hidden <= 1 ? 4 : 2;
-}
+static bool use_flow4(const VissmFlowDesc* d) { return d->n_hidden <= 1; }
 
 static int validate(const VissmFlowDesc* d) {
   VISSM_CHECK_ARG(d, "flow: null desc");
@@ -82,22 +55,10 @@ using namespace vissm;
 
 extern "C" {
 
-int vissm_flow_set_impl(int32_t which) {
-  VISSM_CHECK_ARG(which >= 0 && which <= 4, "flow_set_impl: %d not in [0,4]", which);
-  const int prev = impl_choice();
-  if (which > 0) vissm::g_impl = which;
-  return prev < 0 ? 0 : prev;
-}
-
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
   if (use_v5(d)) return flow5_workspace_size(d, backward);
-  switch (impl_for(d)) {
-    case 1: return flow1_workspace_size(d, backward);
-    case 2: return flow2_workspace_size(d, backward);
-    case 3: return flow3_workspace_size(d, backward);
-    default: return flow4_workspace_size(d, backward);
-  }
+  return use_flow4(d) ? flow4_workspace_size(d, backward) : flow2_workspace_size(d, backward);
 }
 
 int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
@@ -112,12 +73,8 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
   if (use_v5(d)) return flow5_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-  switch (impl_for(d)) {
-    case 1: return flow1_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-    case 2: return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-    case 3: return flow3_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-    default: return flow4_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
-  }
+  if (use_flow4(d)) return flow4_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+  return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
 }
 
 int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
@@ -136,16 +93,9 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
     return flow5_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
-  switch (impl_for(d)) {
-    case 1: return flow1_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                             ws_bytes, st);
-    case 2: return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                             ws_bytes, st);
-    case 3: return flow3_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                             ws_bytes, st);
-    default: return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace,
-                              ws_bytes, st);
-  }
+  if (use_flow4(d))
+    return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
+  return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
 }
 
 }  // extern "C"

@@ -679,48 +679,6 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   }
 }
 
-__global__ void halo_fixup_kernel(float* __restrict__ du, const float* __restrict__ halo, int B, int L, int k,
-                                  int n_chunks, int s, int CH) {
-  const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < (n_chunks - 1) * k; i += blockDim.x) {
-    const int c = i / k, q = i % k;
-    const int pos = s * (c + 1) * CH + q;
-    if (pos < L) du[static_cast<size_t>(b) * L + pos] += halo[(static_cast<size_t>(b) * n_chunks + c) * k + q];
-  }
-}
-
-__global__ void reduce_by_window_kernel(const float* __restrict__ slab, const int32_t* __restrict__ win,
-                                        float* __restrict__ out, int B, int N) {
-  const int wv = blockIdx.y;
-  const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cidx >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b)
-    if (win[b] == wv) s += slab[static_cast<size_t>(b) * N + cidx];
-  out[static_cast<size_t>(wv) * N + cidx] = s;
-}
-
-// scatter the reduced partial into the caller's gradient buffers; d gamma gets the BN scale
-__global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowGrads g, int k, int H, int nh, int bn) {
-  const int nW = k * H + nh * H * H + 3 * nh * H + 2 * H + 2;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nW; i += gridDim.x * blockDim.x) {
-    const float v = red[i];
-    int off = 0;
-    if (i < (off += k * H)) { g.w_eps[i] = v; continue; }
-    if (i < off + nh * H * H) { g.w_hid[i - off] = v; continue; }
-    off += nh * H * H;
-    if (i < off + nh * H) { g.b_hid[i - off] = v; continue; }
-    off += nh * H;
-    if (i < off + nh * H) { if (bn && g.bn_g) g.bn_g[i - off] = v * kBnScale; continue; }
-    off += nh * H;
-    if (i < off + nh * H) { if (bn && g.bn_b) g.bn_b[i - off] = v; continue; }
-    off += nh * H;
-    if (i < off + 2 * H) { g.w_head[i - off] = v; continue; }
-    off += 2 * H;
-    g.b_head[i - off] = v;
-  }
-}
-
 static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   KArgs a;
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.bn = d->bn; a.s = g.s; a.swap_out = d->swap_out;
@@ -810,31 +768,22 @@ int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
               du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow2_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  if (g.n_chunks > 1) {
-    hipLaunchKernelGGL(halo_fixup_kernel, dim3(d->B), dim3(256), 0, st, du, ws.halo, d->B, d->L, d->k, g.n_chunks,
-                       g.s, g.CH);
-    VISSM_CHECK_LAUNCH("flow2_halo");
-  }
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
-  int rc;
   if (d->n_win == 1) {
     rc = launch_reduce_rows(ws.dC_slab, dC, g.n_groups, nC, st);
     if (rc) return rc;
   } else {
-    dim3 rg(static_cast<unsigned>((nC + 255) / 256), d->n_win);
-    hipLaunchKernelGGL(reduce_by_window_kernel, rg, dim3(256), 0, st, ws.dC_slab, win, dC, d->B,
-                       static_cast<int>(nC));
-    VISSM_CHECK_LAUNCH("flow2_reduce_window");
+    rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
+    if (rc) return rc;
   }
   rc = launch_reduce_rows(ws.dth_slab, dtheta_term, g.n_chunks, static_cast<int64_t>(d->B) * d->H, st);
   if (rc) return rc;
   const int nW = n_wgrad(d);
   rc = launch_reduce_rows(ws.dW_slab, ws.wred, static_cast<int64_t>(g.n_groups) * g.n_chunks, nW, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *gr, d->k, d->H,
-                     d->n_hidden, d->bn);
-  VISSM_CHECK_LAUNCH("flow2_scatter");
-  return VISSM_OK;
+  return launch_scatter_wgrad(ws.wred, gr, d->k, d->H, d->n_hidden, d->bn, st);
 }
 
 }  // namespace vissm

@@ -1178,28 +1178,6 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   return a;
 }
 
-// from flow_v4.hip (shared epilogue kernels)
-__global__ void halo_fixup_kernel(float* __restrict__ du, const float* __restrict__ halo, int B, int L, int k,
-                                  int n_chunks, int s, int CH) {
-  const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < (n_chunks - 1) * k; i += blockDim.x) {
-    const int c = i / k, q = i % k;
-    const int pos = s * (c + 1) * CH + q;
-    if (pos < L) du[static_cast<size_t>(b) * L + pos] += halo[(static_cast<size_t>(b) * n_chunks + c) * k + q];
-  }
-}
-
-__global__ void reduce_by_window_kernel(const float* __restrict__ slab, const int32_t* __restrict__ win,
-                                        float* __restrict__ out, int B, int N) {
-  const int wv = blockIdx.y;
-  const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cidx >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b)
-    if (win[b] == wv) s += slab[static_cast<size_t>(b) * N + cidx];
-  out[static_cast<size_t>(wv) * N + cidx] = s;
-}
-
 // Scatter the reduced partials into the caller's gradient buffers, undoing the BN folding:
 // for a layer fed by BN (gamma', beta) the kernel accumulated dWE = sum_p E dZ^T and
 // db = sum_p dZ, so  dW = diag(gamma') dWE + beta db^T,  d gamma' = rowsum(W o dWE),
@@ -1342,21 +1320,15 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
                  dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  if (g.n_chunks > 1) {
-    hipLaunchKernelGGL(flow5::halo_fixup_kernel, dim3(d->B), dim3(256), 0, st, du, ws.halo, d->B, d->L, d->k,
-                       g.n_chunks, g.s, g.CH);
-    VISSM_CHECK_LAUNCH("flow5_halo");
-  }
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
-  int rc;
   if (d->n_win == 1) {
     rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
     if (rc) return rc;
   } else {
-    dim3 rg(static_cast<unsigned>((nC + 255) / 256), d->n_win);
-    hipLaunchKernelGGL(flow5::reduce_by_window_kernel, rg, dim3(256), 0, st, ws.dC_slab, win, dC, d->B,
-                       static_cast<int>(nC));
-    VISSM_CHECK_LAUNCH("flow5_reduce_window");
+    rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
+    if (rc) return rc;
   }
   rc = launch_reduce_rows(ws.dth_slab, dtheta_term, g.n_chunks, static_cast<int64_t>(d->B) * d->H, st);
   if (rc) return rc;
