@@ -7,10 +7,14 @@ A step = window pick -> feature gather -> base noise (Philox) -> 3 IAF flows -> 
 backward -> [RCCL all-reduce] -> global-norm clip + Adamax.  metric = latent-state transitions/s
 = (all ranks' B) * T / step time (weak scaling: B per GPU is fixed).
 
-roofline: the dominant kernel is the IAF-flow backward (flow_bwd_kernel); its algorithmic FLOPs
-per launch divided by its average launch time, measured live with HIP events on
-the launch stream during the timed steps.  cpu_baseline: the fp32 CPU restatement of the same
-step (oracle/, "port") on a bounded sample of trajectories, timed on this host.
+roofline: the dominant kernel is the IAF-flow backward (flow_bwd_kernel); its algorithmic FLOPs per
+launch (2 x F_fwd per sample and head position, SURVEY.md §8d -- the recomputed forward is not
+counted) divided by its average launch time, measured live with HIP events on the launch stream
+during the timed steps; mixed_roof_frac prices the same FLOPs with the vector terms at the fp32
+vector peak.  step_roofline: sum of every kernel's t_min under its own roof / measured step time.
+parity_precision: the same step timed with bf16x3 flow products (ELBO within 1e-4 of the oracle).
+cpu_baseline: the fp32 CPU restatement of the same step (oracle/, "port") on a bounded sample of
+trajectories, timed on this host, plus the AR plumbing config (p = 50, M = 50, k = 50) at true size.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]  (N > 1 under torch.distributed.run)
 """
@@ -32,12 +36,30 @@ METRIC = "latent-state transitions/sec (batch_dims×T per step), AR(1) T=5000, 1
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3}  # MI355X dense (MI355X_MICROARCH.md);
 # bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak
+VALU_PEAK_TFLOPS = 157.3  # fp32 vector (packed FMA) peak
 
 
-def flow_bwd_flops_per_position(k, H, nh):
-    """Algorithmic FLOPs of the flow backward per (sample, head position): recompute forward
-    (2kH + 2 nh H^2 + 4H) + hidden dX and dW (4 nh H^2) + head (8H) + first-layer dW_eps and dU (4kH)."""
-    return 6 * k * H + 6 * nh * H * H + 12 * H
+def flow_fwd_flops_per_position(k, H, nh, bn=False):
+    """SURVEY.md §8(d) algorithmic FLOPs of one flow's forward per (sample, head position):
+    F_fwd = 2kH + 3H + nh (2H^2 + 2H [+ 2H BN]) + 4H + 6.  Returns (F_mfma, F_valu): the nh 2H^2
+    hidden contractions are the matrix-core terms, the rest vector work."""
+    f_mfma = nh * 2 * H * H
+    f_all = 2 * k * H + 3 * H + nh * (2 * H * H + 2 * H + (2 * H if bn else 0)) + 4 * H + 6
+    return f_mfma, f_all - f_mfma
+
+
+def flow_bwd_flops_per_position(k, H, nh, bn=False):
+    """Algorithmic backward FLOPs = 2 F_fwd; the forward the kernel recomputes is
+    not counted (reported separately as recompute_flops_per_launch)."""
+    f_mfma, f_valu = flow_fwd_flops_per_position(k, H, nh, bn)
+    return 2 * (f_mfma + f_valu)
+
+
+def mixed_roof_s(positions, k, H, nh, bn, mfma_peak_tflops, passes):
+    """t_min of `passes` x F_fwd per position with the MFMA terms at the matrix-core peak and the
+    rest at the fp32 vector peak (157.3 TFLOP/s) -- SURVEY.md §8(d)'s roof for the flow kernels."""
+    f_mfma, f_valu = flow_fwd_flops_per_position(k, H, nh, bn)
+    return passes * positions * (f_mfma / (mfma_peak_tflops * 1e12) + f_valu / (VALU_PEAK_TFLOPS * 1e12))
 
 
 def measured_traffic(args):
@@ -57,39 +79,55 @@ def measured_traffic(args):
     return None
 
 
-def cpu_baseline(args, obs, ob, tt):
-    """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories."""
+def _cpu_ar_step_rate(B, M, k, T, obs, ob, tt, seconds, min_steps):
+    """Median seconds per step of the fp32 CPU restatement (oracle/) of the AR step at (B, M, k)."""
     import torch
     from oracle import nma_oracle as O
-    B = min(args.cpu_B, args.B)
-    spec = O.ModelSpec(family="ar", p=B, M=args.M, k=args.k, n_flows=3, H=50, n_layers=3, C_time=14, P_theta=3,
-                       target=float(args.T), priors=[(0.0, 10.0)] * 3, base_loc=1.5, base_scale=0.5)
+    spec = O.ModelSpec(family="ar", p=B, M=M, k=k, n_flows=3, H=50, n_layers=3, C_time=14, P_theta=3,
+                       target=float(T), priors=[(0.0, 10.0)] * 3, base_loc=1.5, base_scale=0.5)
     g = torch.Generator().manual_seed(0)
     params = O.init_params(spec, g, dtype=torch.float32)
     rs = np.random.RandomState(0)
-    starts = rs.choice(np.arange(0, args.T, args.M), size=B, replace=args.M * B >= args.T).tolist()
-    ts = torch.tensor(O.ar_time_feats(obs, ob, tt, 3, args.k, args.M, 10, args.T, starts), dtype=torch.float32)
     leaves = O.param_leaves(params)
     slots = [(torch.zeros_like(t), torch.zeros_like(t)) for t in leaves]
     perms = [[0, 1, 2], [0, 2, 1], [0, 2, 1], [2, 0, 1]]
     times = []
     t_start = time.time()
-    i = 0
     while True:
+        # window draw as AR.py:263-265 (fresh windows every step, like the reference loop)
+        starts = rs.choice(np.arange(0, T, M), size=B, replace=M * B >= T).tolist()
+        ts = torch.tensor(O.ar_time_feats(obs, ob, tt, 3, k, M, 10, T, starts), dtype=torch.float32)
         eps = torch.randn(B, spec.kernel_ext, generator=g)
         x0 = torch.randn(B, 3, generator=g) * 0.5 + 1.5
         t0 = time.perf_counter()
-        new, slots, _ = O.train_step(spec, params, slots, perms, x0, eps, ts, {}, 1e-3, clip=2.5e8)
+        _, slots, _ = O.train_step(spec, params, slots, perms, x0, eps, ts, {}, 1e-3, clip=2.5e8)
         times.append(time.perf_counter() - t0)
-        i += 1
-        if i >= 2 + args.cpu_min_steps or time.time() - t_start > args.cpu_seconds:
+        if len(times) >= 2 + min_steps or time.time() - t_start > seconds:
             break
     steady = times[2:] if len(times) > 2 else times
-    t = float(np.median(steady))
-    return {"value": B * args.M / t, "unit": "transitions/s", "cores": torch.get_num_threads(), "kind": "port",
+    return float(np.median(steady)), len(steady), torch.get_num_threads()
+
+
+def cpu_baseline(args, obs, ob, tt):
+    """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories."""
+    B = min(args.cpu_B, args.B)
+    t, n, cores = _cpu_ar_step_rate(B, args.M, args.k, args.T, obs, ob, tt, args.cpu_seconds, args.cpu_min_steps)
+    return {"value": B * args.M / t, "unit": "transitions/s", "cores": cores, "kind": "port",
             "sample": f"fp32 CPU restatement of the TF1 step (oracle/nma_oracle.py) on B={B} trajectories x "
-                      f"M={args.M} (T={args.T}, k={args.k}), median of {len(steady)} steps after 2 warm-up "
-                      f"({t:.2f} s/step)"}
+                      f"M={args.M} (T={args.T}, k={args.k}), median of {n} steps after 2 warm-up ({t:.2f} s/step)"}
+
+
+def cpu_baseline_ar_plumbing(args):
+    """SURVEY.md §8(d) config 1 at its true size: `python main.py hyperparameters.txt` (p = 50 windows
+    of M = 50, k = 50, data_gen(5000, impute=1, ...) after np.random.seed(1)), fp32 CPU restatement."""
+    from viforssms_amd.data import data_gen
+    np.random.seed(1)
+    obs, ob, tt = data_gen(5000, 1, 10.0, np.array([5.0, 0.5, 3.0]), 1.0, write=False)
+    t, n, cores = _cpu_ar_step_rate(50, 50, 50, 5000, obs, ob, tt, args.cpu_seconds / 2, max(args.cpu_min_steps, 10))
+    return {"value": 50 * 50 / t, "unit": "transitions/s", "cores": cores, "kind": "port",
+            "ms_per_step": t * 1e3,
+            "sample": f"AR plumbing config (hyperparameters.txt: p=50, M=50, k=50, T=5000) at its true size, fp32 CPU "
+                      f"restatement, median of {n} steps after 2 warm-up"}
 
 
 MODEL_DEFAULTS = {  # SURVEY.md §8d configs: per-GPU batch, T, kernel_len
@@ -113,7 +151,7 @@ def build_model(args, ctx, dev, prec):
         theta_spec = build_theta_spec([(0.0, 10.0)] * 3)
         model = VI_SSM(obs, 1.0, 10.0, theta_spec, [(0.0, 10.0)] * 3, args.T, p_global, args.k, args.M, [50, 50, 50],
                        3, 10, ob, tt, pre_train=False, learn_rate=1e-3, grad_clip=2.5e8, **common)
-        meta = dict(D=1, nh=1, n_flows=3, ar_data=(obs, ob, tt),
+        meta = dict(D=1, nh=1, n_flows=3, bn=False, ar_data=(obs, ob, tt),
                     data="synthetic: AR(1) series from data_gen(5000, impute=5, x0=10, theta=[5,.5,3], obs_std=1) "
                          "after np.random.seed(1); random-init (glorot) weights; base noise from Philox",
                     workload=f"AR(1) ELBO train step, T={args.T}, M={args.M}, impute=5, kernel_len={args.k}, no_flows=3, "
@@ -127,7 +165,7 @@ def build_model(args, ctx, dev, prec):
         spec = ThetaSpec.build(4, 5, 0.0, 1.0, "relu")
         model = VI_SSM(obs, -8.5, spec, [(0.0, 10.0)] * 4, 1.0, args.T, p_global, args.k, args.T, [50] * 5, args.T,
                        5, 5, learn_rate=1e-4, pre_train=False, **common)
-        meta = dict(D=1, nh=3, n_flows=5, data="dat/SV.dat[300:] (the reference's series); random-init weights",
+        meta = dict(D=1, nh=3, n_flows=5, bn=True, data="dat/SV.dat[300:] (the reference's series); random-init weights",
                     workload=f"SV ELBO train step (SV_dense.py), T=M={args.T}, kernel_len={args.k}, no_flows=5, "
                              f"network_dims=[50]*5, feat_window=5, B={args.B} per GPU")
     elif args.model == "lv":
@@ -138,7 +176,7 @@ def build_model(args, ctx, dev, prec):
         spec = ThetaSpec.build(3, 4, 0.0, 1.0, "elu")
         model = VI_SSM(obs, ob, tt, np.array([100.0, 100.0]), spec, PRIORS, 0.1, args.T * 0.1, p_global, args.k,
                        args.T, [50] * 5, args.T, 3, 10, pre_train=False, **common)
-        meta = dict(D=2, nh=3, n_flows=3,
+        meta = dict(D=2, nh=3, n_flows=3, bn=True,
                     data="synthetic: Euler-Maruyama LV path theta=(0.5,0.0025,0.3), x0=(100,100), dt=0.1, obs N(x,1) "
                          "every 100 steps; random-init weights",
                     workload=f"Lotka-Volterra ELBO train step (lotka_volterra_partial.py), T=M={args.T}, "
@@ -151,7 +189,7 @@ def build_model(args, ctx, dev, prec):
         spec = ThetaSpec.build(5, 4, 0.0, 1.0, "elu")
         model = VI_SSM(obs, ob, tt, np.array([2.0, 3.0]), spec, [(0.0, 10.0)] * 5, 0.1, args.T * 0.1, p_global,
                        args.k, args.T, [50] * 5, args.T, 3, 10, pre_train=False, **common)
-        meta = dict(D=2, nh=3, n_flows=3,
+        meta = dict(D=2, nh=3, n_flows=3, bn=True,
                     data="synthetic: Euler-Maruyama FHN path, x0=(2,3), dt=0.1, obs N(x,0.1) every 10 steps; "
                          "random-init weights",
                     workload=f"FitzHugh-Nagumo ELBO train step (fitz_nag_NVP.py), T=M={args.T}, kernel_len={args.k}, "
@@ -179,6 +217,8 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured HIP graph (viforssms_amd.graph; needs warmup >= 3)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--parity-line", choices=["auto", "off"], default="auto",
+                    help="also time the step at bf16x3 (AR, bf16, 1 GPU) and report it as parity_precision")
     ap.add_argument("--cpu-B", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--cpu-min-steps", type=int, default=5)
@@ -213,54 +253,74 @@ def main():
     if args.graph:
         args.warmup = max(args.warmup, 3)  # two eager warm-up steps, then the capture
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+    def timed(first_step):
+        """Warm-up, then EXACTLY args.steps timed steps between barrier + synchronize on both sides;
+        max over ranks.  Returns (elapsed_s, {profile kind: (ms, launches, algorithmic bytes)})."""
+        for i in range(args.warmup):
+            step(first_step + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        lib.vissm_profile_reset()
+        lib.vissm_profile_enable(1)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(first_step + args.warmup + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        lib.vissm_profile_enable(0)
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        tot, cnt, nbytes = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        prof = {}
+        for kind in (_lib.PROF_FLOW_FWD, _lib.PROF_FLOW_BWD, _lib.PROF_ELBO_FWD, _lib.PROF_ELBO_BWD, _lib.PROF_NORMAL):
+            _lib.check(lib.vissm_profile_read(kind, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
+            _lib.check(lib.vissm_profile_bytes(kind, ctypes.byref(nbytes)), "profile_bytes")
+            prof[kind] = (tot.value, cnt.value, nbytes.value)
+        lib.vissm_profile_reset()
+        return elapsed, prof
+
+    import ctypes
     if world > 1:
         import torch.distributed as dist
-        dist.barrier()
-    lib.vissm_profile_reset()
-    lib.vissm_profile_enable(1)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    lib.vissm_profile_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    import ctypes
-    tot = ctypes.c_double()
-    cnt = ctypes.c_int64()
-    _lib.check(lib.vissm_profile_read(_lib.PROF_FLOW_BWD, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
-    bwd_ms, bwd_n = tot.value, cnt.value
-    _lib.check(lib.vissm_profile_read(_lib.PROF_FLOW_FWD, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
-    fwd_ms, fwd_n = tot.value, cnt.value
-    stream_ms = {}
-    nbytes = ctypes.c_double()
-    for kind in (_lib.PROF_ELBO_FWD, _lib.PROF_ELBO_BWD, _lib.PROF_NORMAL):
-        _lib.check(lib.vissm_profile_read(kind, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
-        _lib.check(lib.vissm_profile_bytes(kind, ctypes.byref(nbytes)), "profile_bytes")
-        stream_ms[kind] = (tot.value, cnt.value, nbytes.value)
-    lib.vissm_profile_reset()
+    elapsed, prof = timed(0)
+    # parity-precision line: the same step with bf16x3 flow products (the precision that holds the
+    # per-sample ELBO within north_star's 1e-4 of the float64 oracle), timed the same way
+    px = None
+    if args.parity_line == "auto" and args.precision == "bf16" and args.model == "ar" and world == 1 and not args.graph:
+        model.engine.precision = _lib.VISSM_PREC_BF16X3
+        px_elapsed, px_prof = timed(args.warmup + args.steps)
+        model.engine.precision = prec
+        b_ms, b_n, _ = px_prof[_lib.PROF_FLOW_BWD]
+        f_ms, f_n, _ = px_prof[_lib.PROF_FLOW_FWD]
+        px = {"dtype": "bf16x3", "value": world * args.B * args.M * args.steps / px_elapsed,
+              "ms_per_step": px_elapsed / args.steps * 1e3, "flow_bwd_avg_ms": b_ms / max(b_n, 1),
+              "flow_fwd_avg_ms": f_ms / max(f_n, 1),
+              "note": "same workload, flow MFMA operands split bf16 hi+lo (three products): per-sample ELBO within "
+                      "1e-4 of the float64 oracle (tests/test_gpu_config_parity.py)"}
 
     if rank != 0:
         return
-    B, T, k, H, nh, nf, D = args.B, args.M, args.k, 50, meta["nh"], meta["n_flows"], meta["D"]
+    B, T, k, H, nh, nf, D, bn = args.B, args.M, args.k, 50, meta["nh"], meta["n_flows"], meta["D"], meta["bn"]
     kext = nf * k + D * T + D
     Lh = [(kext - i * k - k) // D for i in range(nf)]
-    fl_pos = flow_bwd_flops_per_position(k, H, nh)
-    flops_per_launch = B * fl_pos * sum(Lh) / nf
+    positions_per_launch = B * sum(Lh) / nf
+    fwd_ms, fwd_n, _ = prof[_lib.PROF_FLOW_FWD]
+    bwd_ms, bwd_n, _ = prof[_lib.PROF_FLOW_BWD]
+    flops_per_launch = positions_per_launch * flow_bwd_flops_per_position(k, H, nh, bn)
     avg_launch_s = bwd_ms / max(bwd_n, 1) / 1e3
     achieved = flops_per_launch / avg_launch_s / 1e12 if bwd_n else None
     peak = PEAKS_TFLOPS[args.precision]
     kernel = "flow5::bwd_kernel (bf16 matrix cores)" if args.precision != "fp32" else "flow4::bwd_kernel (fp32 matrix cores)"
     traffic = measured_traffic(args)
+    t_step = elapsed / args.steps
     value = world * B * T * args.steps / elapsed
+    mfma_peak = PEAKS_TFLOPS[args.precision] if args.precision != "fp32" else VALU_PEAK_TFLOPS
+    bwd_roof_s = mixed_roof_s(positions_per_launch, k, H, nh, bn, mfma_peak, 2)
     res = {
         "metric": METRIC if args.model == "ar" else METRIC.replace("AR(1) T=5000", f"{args.model.upper()} T={T}"),
         "value": value,
@@ -268,7 +328,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": t_step * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -279,7 +339,12 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                      "kernel": kernel, "flops_per_launch": flops_per_launch,
+                     "flops_accounting": "2 x F_fwd per (sample, head position), SURVEY.md §8(d); "
+                                         "the recomputed forward is not counted",
+                     "recompute_flops_per_launch": flops_per_launch / 2,
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
+                     "mixed_roof_ms": bwd_roof_s * 1e3,
+                     "mixed_roof_frac": bwd_roof_s / avg_launch_s if bwd_n else None,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
     }
     # the HBM-bound streaming kernels of the step: the algorithmic bytes each launch
@@ -290,15 +355,33 @@ def main():
              _lib.PROF_NORMAL: "normal_base_kernel (Philox base noise: writes eps)"}
     streaming = []
     for kind, name in names.items():
-        ms, n, nb = stream_ms[kind]
+        ms, n, nb = prof[kind]
         if n and ms > 0:
             gbs = nb / (ms / 1e3) / 1e9
             streaming.append({"kernel": name, "bound": "hbm", "bytes_per_launch": nb / n, "avg_launch_ms": ms / n,
                               "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                               "launches": n})
     res["streaming_rooflines"] = streaming
+    # SURVEY.md §8(d) step-level accounting: sum over the step's kernels of each one's t_min under its own
+    # roof (flows: MFMA terms at the matrix-core peak + vector terms at 157.3 TF; streaming kernels: their
+    # algorithmic bytes at 8 TB/s; Adamax: 32 B/param), divided by the measured step time
+    terms = {
+        "flow_fwd": mixed_roof_s(positions_per_launch, k, H, nh, bn, mfma_peak, 1) * nf,
+        "flow_bwd": bwd_roof_s * nf,
+        "adamax": 32.0 * model.store.numel / (HBM_PEAK_GBS * 1e9),
+    }
+    for kind, key in ((_lib.PROF_ELBO_FWD, "elbo_fwd"), (_lib.PROF_ELBO_BWD, "elbo_bwd"), (_lib.PROF_NORMAL, "base_noise")):
+        ms, n, nb = prof[kind]
+        terms[key] = (nb / args.steps) / (HBM_PEAK_GBS * 1e9)
+    t_min = sum(terms.values())
+    res["step_roofline"] = {"t_min_ms": t_min * 1e3, "t_step_ms": t_step * 1e3, "frac": t_min / t_step,
+                            "terms_ms": {kk: v * 1e3 for kk, v in terms.items()},
+                            "note": "sum of per-kernel t_min (SURVEY.md §8d) / measured step time"}
+    if px is not None:
+        res["parity_precision"] = px
     if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
         res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
+        res["cpu_baseline"]["ar_plumbing"] = cpu_baseline_ar_plumbing(args)
     else:
         res["cpu_baseline"] = None
     print(json.dumps(res), flush=True)
