@@ -188,6 +188,15 @@ int vissm_adamax_step(float* params, const float* grads, float* v, float* m,
                       float clip, float* gnorm_out, void* workspace,
                       size_t ws_bytes, void* stream);
 
+/* As vissm_adamax_step, with the non-finite guard of the training loop: when ||g||
+ * is not finite -- where tf.clip_by_global_norm would write NaN into every variable
+ * (AR.py:230-232) -- params, v and m are left untouched and *skipped (device int32, may be NULL)
+ * is incremented.  The decision is made on the device: no host synchronisation. */
+int vissm_adamax_step_guarded(float* params, const float* grads, float* v, float* m,
+                              int64_t n, float lr, float beta1, float beta2, float eps,
+                              float clip, float* gnorm_out, int32_t* skipped, void* workspace,
+                              size_t ws_bytes, void* stream);
+
 /* Sum of squares of a flat buffer (fixed-order), result to out[0] (device float). */
 int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace,
                  size_t ws_bytes, void* stream);
@@ -195,6 +204,27 @@ int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace,
 /* out[c] = sum_r slab[r][c] for r = 0..R-1 in fixed order (deterministic reduce). */
 int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N,
                       void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;
+ * lotka_volterra_partial.py:366-386; SV_dense.py:304-328) from device-resident
+ * padded channel tables (built once, AR.py:135-150), keyed by the step's window
+ * starts (batch_select):
+ *   out[r*os_r + j*os_j + c*os_c] = src[c*c_pitch + stride*starts[r] + offset + j*j_step]
+ * for r < n, j < len, c < C.  time_feats [n][kernel_ext][C]: c_pitch = table
+ * length, os = (kernel_ext*C, C, 1); per-window feeds [n][D][len] from a [D][..]
+ * table: os = (D*len, 1, len).  The caller guarantees every source index lies in
+ * the table (the reference's starts come from arange(0, T, M)).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t n, len, C;        /* windows, positions per window, channels */
+  int32_t stride;           /* start multiplier (2 for the interleaved 2-D series) */
+  int64_t offset, j_step, c_pitch;
+  int64_t os_r, os_j, os_c; /* output strides (elements) */
+} VissmGatherDesc;
+
+int vissm_gather_windows(const VissmGatherDesc* d, const float* src, const int32_t* starts,
+                         float* out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Opt-in kernel timing (for bench.py's live roofline): when enabled, the flow

@@ -74,3 +74,24 @@ def test_all_windows_batch_matches_distinct_windows(family, B, M, k, nf, H, nl, 
     assert torch.allclose(eb, ea, rtol=1e-5, atol=1e-5 * float(ea.abs().mean()))
     ga, gb = a.store.grad.double(), b.store.grad.double()
     assert float((ga - gb).norm() / ga.norm()) < 1e-5
+
+
+def test_graph_steps_without_synchronize_match_synchronized_steps():
+    """Replays issued back to back (the host runs ahead of the GPU, as bench.py --graph and main.py
+    --graph do) give bitwise the same ELBOs and parameters as replays with a synchronize after every
+    step: each step's window map reaches the GPU before the host stages the next one."""
+    family, B, M, k, nf, H, nl, fw, T, prec = CASES[0]
+    a, b = _pair(family, B, M, k, nf, H, nl, fw, T, prec)
+    rng = np.random.default_rng(11)
+    universe = np.arange(0, a.target_len(), M)
+    draws = [rng.choice(universe, size=B, replace=True) for _ in range(10)]
+    ea, eb = [], []
+    for step, starts in enumerate(draws):
+        ea.append(a.graphed_step(starts, step)["elbo"].clone())   # stream-ordered copy, no host sync
+    for step, starts in enumerate(draws):
+        eb.append(b.graphed_step(starts, step)["elbo"].clone())
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for step, (x, y) in enumerate(zip(ea, eb)):
+        assert torch.equal(x, y), step
+    assert torch.equal(a.store.flat, b.store.flat)

@@ -45,6 +45,11 @@ class ElboDesc(ctypes.Structure):
     _fields_ = [("model", _i32), ("B", _i32), ("M", _i32), ("n_win", _i32), ("dt", _f32), ("obs_std", _f32)]
 
 
+class GatherDesc(ctypes.Structure):
+    _fields_ = [("n", _i32), ("len", _i32), ("C", _i32), ("stride", _i32), ("offset", _i64), ("j_step", _i64),
+                ("c_pitch", _i64), ("os_r", _i64), ("os_j", _i64), ("os_c", _i64)]
+
+
 class ElboData(ctypes.Structure):
     _fields_ = [(n, _c_void_p) for n in ("win", "obs", "obs_bin", "mask", "shift", "dim_one")]
 
@@ -69,8 +74,11 @@ SIGNATURES = {
     "vissm_adamax_workspace_size": (_size_t, [_i64]),
     "vissm_adamax_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
                                  _f32, _c_void_p, _c_void_p, _size_t, _c_void_p]),
+    "vissm_adamax_step_guarded": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
+                                         _f32, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
+    "vissm_gather_windows": (_i32, [ctypes.POINTER(GatherDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_profile_enable": (None, [_i32]),
     "vissm_profile_read": (_i32, [_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "vissm_profile_reset": (None, []),

@@ -215,9 +215,12 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __rest
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// skip (guarded step only, may be NULL): set to 1 when the norm is not finite, else 0; *skipped counts
+// the skipped steps
 __global__ __launch_bounds__(1024) void sqnorm_final_kernel(const double* __restrict__ part, int np,
                                                             float* __restrict__ sq_out, float* __restrict__ norm_out,
-                                                            float* __restrict__ scale_out, float clip) {
+                                                            float* __restrict__ scale_out, float clip,
+                                                            int32_t* __restrict__ skip, int32_t* __restrict__ skipped) {
   __shared__ double red[16];
   double v = threadIdx.x < np ? part[threadIdx.x] : 0.0;
   double s = block_sum(v, red);
@@ -233,13 +236,19 @@ __global__ __launch_bounds__(1024) void sqnorm_final_kernel(const double* __rest
       else sc = static_cast<float>(static_cast<double>(clip) * fmin(1.0 / nrm, 1.0 / static_cast<double>(clip)));
       *scale_out = sc;
     }
+    if (skip) {
+      const int bad = isfinite(nrm) ? 0 : 1;
+      skip[0] = bad;
+      if (skipped) skipped[0] += bad;
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void adamax_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                      float* __restrict__ v, float* __restrict__ m, int64_t n,
                                                      const float* __restrict__ scale_ptr, float lr, float b1,
-                                                     float b2, float eps) {
+                                                     float b2, float eps, const int32_t* __restrict__ skip) {
+  if (skip && skip[0]) return;  // guarded step with a non-finite norm: params and slots untouched
   const float sc = *scale_ptr;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -341,13 +350,15 @@ size_t vissm_adamax_workspace_size(int64_t n) {
 }
 
 static int sqnorm_impl(const float* x, int64_t n, float* sq_out, float* norm_out, float* scale_out, float clip,
-                       void* ws, size_t ws_bytes, hipStream_t st) {
+                       void* ws, size_t ws_bytes, hipStream_t st, int32_t* skip = nullptr,
+                       int32_t* skipped = nullptr) {
   VISSM_CHECK_ARG(ws && ws_bytes >= vissm_adamax_workspace_size(n), "workspace too small");
   double* part = reinterpret_cast<double*>(ws);
   int nb = static_cast<int>(std::min<int64_t>(kNormBlocks, std::max<int64_t>(1, (n + 1023) / 1024)));
   hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, x, n, part);
   VISSM_CHECK_LAUNCH("sqnorm_partial");
-  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(1024), 0, st, part, nb, sq_out, norm_out, scale_out, clip);
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(1024), 0, st, part, nb, sq_out, norm_out, scale_out, clip,
+                     skip, skipped);
   VISSM_CHECK_LAUNCH("sqnorm_final");
   return VISSM_OK;
 }
@@ -357,20 +368,37 @@ int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace, size_t 
   return sqnorm_impl(x, n, out, nullptr, nullptr, 0.f, workspace, ws_bytes, as_stream(stream));
 }
 
-int vissm_adamax_step(float* params, const float* grads, float* v, float* m, int64_t n, float lr, float beta1,
-                      float beta2, float eps, float clip, float* gnorm_out, void* workspace, size_t ws_bytes,
-                      void* stream) {
+static int adamax_impl(float* params, const float* grads, float* v, float* m, int64_t n, float lr, float beta1,
+                       float beta2, float eps, float clip, float* gnorm_out, bool guard, int32_t* skipped,
+                       void* workspace, size_t ws_bytes, hipStream_t st) {
   VISSM_CHECK_ARG(params && grads && v && m && n >= 0, "adamax_step: bad args");
-  hipStream_t st = as_stream(stream);
+  // workspace: [norm partials (doubles)] [scale, norm scratch, skip flag]
   float* scratch = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + align_up(kNormBlocks * sizeof(double)));
-  int rc = sqnorm_impl(grads, n, nullptr, gnorm_out ? gnorm_out : scratch + 1, scratch, clip, workspace, ws_bytes, st);
+  int32_t* skip = guard ? reinterpret_cast<int32_t*>(scratch + 2) : nullptr;
+  int rc = sqnorm_impl(grads, n, nullptr, gnorm_out ? gnorm_out : scratch + 1, scratch, clip, workspace, ws_bytes, st,
+                       skip, skipped);
   if (rc) return rc;
   int nb = static_cast<int>(std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)));
   hipLaunchKernelGGL(adamax_kernel, dim3(nb), dim3(256), 0, st, params, grads, v, m, n, scratch, lr, beta1, beta2,
-                     eps);
+                     eps, skip);
   VISSM_CHECK_LAUNCH("adamax");
   return VISSM_OK;
 }
+
+int vissm_adamax_step(float* params, const float* grads, float* v, float* m, int64_t n, float lr, float beta1,
+                      float beta2, float eps, float clip, float* gnorm_out, void* workspace, size_t ws_bytes,
+                      void* stream) {
+  return adamax_impl(params, grads, v, m, n, lr, beta1, beta2, eps, clip, gnorm_out, false, nullptr, workspace,
+                     ws_bytes, as_stream(stream));
+}
+
+int vissm_adamax_step_guarded(float* params, const float* grads, float* v, float* m, int64_t n, float lr,
+                              float beta1, float beta2, float eps, float clip, float* gnorm_out, int32_t* skipped,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  return adamax_impl(params, grads, v, m, n, lr, beta1, beta2, eps, clip, gnorm_out, true, skipped, workspace,
+                     ws_bytes, as_stream(stream));
+}
+
 
 void vissm_profile_enable(int32_t on) { vissm::g_prof = on != 0; }
 

@@ -131,3 +131,66 @@ def sv_table(obs, x0, T, dt, target_dims, n_flows, k, M, fw) -> FeatureTable:
     kext = n_flows * k + M + 1
     return FeatureTable("sv", M, kext, chans, 1, {"mask_vals": mask_vals, "shift_vals": shift_vals,
                                                    "obs": np.asarray(obs, dtype=np.float64)})
+
+
+class DeviceTable:
+    """The FeatureTable's padded channel arrays (and the per-window feed tables) resident on the GPU,
+    built once per model; ``batch(uniq_dev, n)`` gathers time_feats and the ELBO feeds of n window
+    starts with vissm_gather_windows -- the step's only upload is its int32 window starts."""
+
+    def __init__(self, tab: FeatureTable, device):
+        import torch
+        self.tab = tab
+        self.device = device
+        f32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=device)
+        Lmax = max(len(c) for c in tab.chans)
+        chans = np.zeros((tab.C, Lmax), dtype=np.float32)
+        for c, arr in enumerate(tab.chans):
+            chans[c, :len(arr)] = arr
+        self.chans = f32(chans)
+        self.pitch = Lmax
+        ex = tab.extra
+        self.extra = {}
+        if tab.family in ("lv", "fhn"):
+            self.extra["obs_bin"] = f32(ex["obs_bin"])
+        if tab.family in ("lv", "sv"):
+            self.extra["mask"] = f32(ex["mask_vals"])
+            self.extra["shift"] = f32(ex["shift_vals"])
+        if tab.family == "sv":
+            self.extra["dim_one"] = f32(np.asarray(ex["obs"]).reshape(1, -1))
+
+    def batch(self, uniq_dev, n: int):
+        """(ts [n, kext, C], feeds dict) for the window starts uniq_dev (int32 [n] on the device)."""
+        import torch
+        from .ops import gather_windows
+        t, M, K, C = self.tab, self.tab.M, self.tab.kext, self.tab.C
+        dev = self.device
+        ts = torch.empty(n, K, C, dtype=torch.float32, device=dev)
+        gather_windows(self.chans, uniq_dev, ts, n, K, C, stride=t.stride, c_pitch=self.pitch, os=(K * C, C, 1))
+        feeds = {}
+        if t.family == "ar":                                      # AR.py:155, AR.py:170
+            for key, ch in (("obs", 0), ("obs_bin", C - 1)):
+                out = torch.empty(n, M, dtype=torch.float32, device=dev)
+                gather_windows(self.chans[ch], uniq_dev, out, n, M, 1, offset=K - M, os=(M, 1, 0))
+                feeds[key] = out
+        elif t.family in ("lv", "fhn"):                           # lotka_volterra_partial.py:218-219, 385-386
+            out = torch.empty(n, 2, M, dtype=torch.float32, device=dev)
+            gather_windows(self.chans[0], uniq_dev, out, n, M, 2, stride=2, offset=K - 2 * M, j_step=2, c_pitch=1,
+                           os=(2 * M, 1, M))
+            feeds["obs"] = out
+            ob = self.extra["obs_bin"]
+            out = torch.empty(n, 2, M, dtype=torch.float32, device=dev)
+            gather_windows(ob, uniq_dev, out, n, M, 2, c_pitch=ob.shape[1], os=(2 * M, 1, M))
+            feeds["obs_bin"] = out
+        if t.family in ("lv", "sv"):                              # lotka_volterra_partial.py:381-384, SV_dense.py:322-328
+            D = 2 if t.family == "lv" else 1
+            for key in ("mask", "shift"):
+                tab = self.extra[key]
+                out = torch.empty((n, D, M + 1) if D == 2 else (n, M + 1), dtype=torch.float32, device=dev)
+                gather_windows(tab, uniq_dev, out, n, M + 1, D, c_pitch=tab.shape[1], os=(D * (M + 1), 1, M + 1))
+                feeds[key] = out
+        if t.family == "sv":
+            out = torch.empty(n, M + 1, dtype=torch.float32, device=dev)
+            gather_windows(self.extra["dim_one"], uniq_dev, out, n, M + 1, 1, os=(M + 1, 1, 0))
+            feeds["dim_one"] = out
+        return ts, feeds

@@ -39,7 +39,11 @@ class GraphedStep:
         self.win: Optional[torch.Tensor] = None
         if len(self.universe) > 1:
             self.win = torch.zeros(B, dtype=torch.int32, device=dev)
-            self._win_host = torch.zeros(B, dtype=torch.int32).pin_memory()
+            # two pinned staging buffers, each reused only after the event behind its last copy has
+            # completed: the host may run steps ahead of the GPU (no per-step synchronize)
+            self._win_host = [torch.zeros(B, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._win_done = [None, None]
+            self._slot = 0
         feeds = dataclasses.replace(base.feeds, win=self.win, n_win=len(self.universe))
         self.batch = Batch(np.zeros(B, dtype=np.int64), base.uniq, base.ts, self.win, feeds, base.host_feeds)
         self.row0 = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -56,8 +60,14 @@ class GraphedStep:
             idx = np.searchsorted(self.universe, local)
             if not np.array_equal(self.universe[idx], local):
                 raise ValueError("window start outside arange(0, T, M)")
-            self._win_host.numpy()[:] = idx.astype(np.int32)
-            self.win.copy_(self._win_host, non_blocking=True)
+            i, self._slot = self._slot, self._slot ^ 1
+            if self._win_done[i] is not None:
+                self._win_done[i].synchronize()
+            self._win_host[i].numpy()[:] = idx.astype(np.int32)
+            self.win.copy_(self._win_host[i], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._win_done[i] = ev
         self.row0.fill_(step * m.p + r * pl)
 
     def step(self, starts_global: np.ndarray, step: int) -> Dict[str, torch.Tensor]:

@@ -300,8 +300,13 @@ class Engine:
 
     # ---- batches ----
     def make_batch(self, starts: np.ndarray) -> Batch:
+        """The step's batch for reference window starts `starts` (batch_select): on the GPU the windows
+        are gathered from the device-resident tables (features.DeviceTable, vissm_gather_windows) and
+        only the int32 starts are uploaded; on a CPU device (host-side tests) the host gather runs."""
         starts = np.asarray(starts, dtype=np.int64)
         uniq, inv = np.unique(starts, return_inverse=True)
+        if self.device.type == "cuda":
+            return self._make_batch_device(starts, uniq, inv)
         ts_np = self.table.windows(uniq)
         feeds_np = self.table.feeds(uniq, ts_np)
         dev = self.device
@@ -314,6 +319,19 @@ class Engine:
                           dim_one=t(feeds_np["dim_one"]) if "dim_one" in feeds_np else None,
                           win=win, n_win=len(uniq))
         return Batch(starts, uniq, t(ts_np), win, feeds, feeds_np)
+
+    def _make_batch_device(self, starts, uniq, inv) -> Batch:
+        if getattr(self, "_dtab", None) is None:
+            from .features import DeviceTable
+            self._dtab = DeviceTable(self.table, self.device)
+        n = len(uniq)
+        idx = np.concatenate([uniq, inv]).astype(np.int32) if n > 1 else uniq.astype(np.int32)
+        idx_dev = torch.from_numpy(idx).to(self.device)
+        ts, f = self._dtab.batch(idx_dev[:n], n)
+        win = idx_dev[n:] if n > 1 else None
+        feeds = ElboFeeds(obs=f.get("obs"), obs_bin=f.get("obs_bin"), mask=f.get("mask"), shift=f.get("shift"),
+                          dim_one=f.get("dim_one"), win=win, n_win=n)
+        return Batch(starts, uniq, ts, win, feeds, {})
 
     # ---- random inputs (Philox; keyed by global sample index so sharding is exact) ----
     def draw(self, step: int, B: int, global_offset: int, B_total: int, row0_dev: Optional[torch.Tensor] = None):
@@ -416,11 +434,14 @@ class ScalarLog:
             os.makedirs(d, exist_ok=True)
             self.f = open(os.path.join(d, "scalars.jsonl"), "a")
 
-    def write(self, run: int, values: Dict[str, float]):
+    def write(self, run: int, values: Dict[str, float], histograms: Optional[Dict[str, Dict]] = None):
         if self.f is None:
             return
         import json
-        self.f.write(json.dumps({"step": run, **{k: float(v) for k, v in values.items()}}) + "\n")
+        rec = {"step": run, **{k: float(v) for k, v in values.items()}}
+        if histograms:
+            rec["histograms"] = histograms
+        self.f.write(json.dumps(rec) + "\n")
         self.f.flush()
 
     def close(self):

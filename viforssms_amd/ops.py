@@ -14,7 +14,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import FlowDesc, FlowParams, FlowGrads, ElboDesc, ElboData, check, ptr
+from ._lib import FlowDesc, FlowParams, FlowGrads, ElboDesc, ElboData, GatherDesc, check, ptr
 
 
 def _require_gpu(*ts):
@@ -68,6 +68,23 @@ def base_logprob(eps: torch.Tensor, n_last: int) -> torch.Tensor:
     check(lib.vissm_base_logprob(ptr(eps), ptr(lp), B, L, n_last, _lib.stream_handle(eps.device)),
           "vissm_base_logprob")
     return lp
+
+
+# ---------------------------------------------------------------------------------------
+# window gather
+# ---------------------------------------------------------------------------------------
+def gather_windows(src: torch.Tensor, starts: torch.Tensor, out: torch.Tensor, n: int, length: int, C: int,
+                   stride: int = 1, offset: int = 0, j_step: int = 1, c_pitch: int = 0, os=None) -> torch.Tensor:
+    """out[r*os_r + j*os_j + c*os_c] = src.flat[c*c_pitch + stride*starts[r] + offset + j*j_step]
+    (vissm_gather_windows: the train loop's window gather, AR.py:267-288, from a device-resident table)."""
+    _require_gpu(src, starts, out)
+    if starts.dtype != torch.int32 or src.dtype != torch.float32:
+        raise _lib.VissmError("gather_windows: int32 starts and fp32 tables expected")
+    os_r, os_j, os_c = os
+    d = GatherDesc(n, length, C, stride, offset, j_step, c_pitch, os_r, os_j, os_c)
+    check(_lib.load().vissm_gather_windows(ctypes.byref(d), ptr(src), ptr(starts), ptr(out),
+                                           _lib.stream_handle(src.device)), "vissm_gather_windows")
+    return out
 
 
 # ---------------------------------------------------------------------------------------
@@ -238,13 +255,22 @@ class AdamaxKernel:
         self.wsz = lib.vissm_adamax_workspace_size(n)
         self.ws = _workspace(self.wsz, device)
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=device)
+        self.skipped = torch.zeros(1, dtype=torch.int32, device=device)  # guarded steps skipped so far
 
-    def step(self, params, grads, v, m, lr, beta1, beta2, eps=1e-8, clip=0.0):
+    def step(self, params, grads, v, m, lr, beta1, beta2, eps=1e-8, clip=0.0, guard=False):
+        """guard: skip the update (params and slots untouched, self.skipped += 1) when the global norm
+        is not finite, instead of the reference's NaN-everything (vissm_adamax_step_guarded)."""
         lib = _lib.load()
         _require_gpu(params, grads, v, m)
-        check(lib.vissm_adamax_step(ptr(params), ptr(grads), ptr(v), ptr(m), self.n, float(lr), float(beta1),
-                                    float(beta2), float(eps), float(clip), ptr(self.gnorm), ptr(self.ws), self.wsz,
-                                    _lib.stream_handle(params.device)), "vissm_adamax_step")
+        if guard:
+            check(lib.vissm_adamax_step_guarded(ptr(params), ptr(grads), ptr(v), ptr(m), self.n, float(lr),
+                                                float(beta1), float(beta2), float(eps), float(clip), ptr(self.gnorm),
+                                                ptr(self.skipped), ptr(self.ws), self.wsz,
+                                                _lib.stream_handle(params.device)), "vissm_adamax_step_guarded")
+        else:
+            check(lib.vissm_adamax_step(ptr(params), ptr(grads), ptr(v), ptr(m), self.n, float(lr), float(beta1),
+                                        float(beta2), float(eps), float(clip), ptr(self.gnorm), ptr(self.ws), self.wsz,
+                                        _lib.stream_handle(params.device)), "vissm_adamax_step")
         return self.gnorm
 
 

@@ -64,7 +64,7 @@ class VISSMBase:
     def __init__(self, mdef: ModelDef, table, theta_spec: ThetaSpec, p: int, pre_train: bool,
                  early_stopping: float, learn_rate: float, grad_clip: float, device=None, seed: int = 1,
                  precision: int = _lib.VISSM_PREC_FP32, dist: Optional[DistCtx] = None, log_every: int = 1,
-                 init_seed: int = 1):
+                 init_seed: int = 1, skip_nonfinite: bool = True):
         mdef.n_maf = theta_spec.n_bijectors
         mdef.theta_base = (theta_spec.base_loc, theta_spec.base_scale)
         mdef.theta_act = theta_spec.activation
@@ -82,6 +82,10 @@ class VISSMBase:
         self.learn_rate = learn_rate
         self.grad_clip = grad_clip
         self.log_every = max(1, int(log_every))
+        # SURVEY.md §5 failure detection: a step whose all-reduced global norm is not finite is skipped on
+        # the device (params and slots untouched) and counted in optimize/skipped_steps; False restores the
+        # reference's clip_by_global_norm behaviour (NaN written into every variable, AR.py:230-232)
+        self.skip_nonfinite = bool(skip_nonfinite)
         self.T = mdef.scale_num
         self.batch_dims = mdef.M
         self._batch_cache: Dict[tuple, Batch] = {}
@@ -154,7 +158,8 @@ class VISSMBase:
         self._reduce_grads()
         if apply:
             o = self._opt_main
-            gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm())
+            gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm(),
+                               guard=self.skip_nonfinite)
             out["global_norm"] = gn
         return out
 
@@ -219,6 +224,8 @@ class VISSMBase:
         }
         if "global_norm" in out:
             vals["optimize/global_norm"] = out["global_norm"][0]
+            if self.skip_nonfinite and self._opt_main is not None:
+                vals["optimize/skipped_steps"] = self._opt_main.kernel.skipped[0]
         keys = list(vals)
         stacked = torch.stack([v.detach().float().reshape(()) for v in vals.values()])
         if self.dist.world > 1:
@@ -226,7 +233,37 @@ class VISSMBase:
             self.dist.all_reduce_(stacked)
             stacked = stacked / self.dist.world
         host = stacked.cpu().numpy()
-        return {k: float(v) for k, v in zip(keys, host)}
+        res = {k: float(v) for k, v in zip(keys, host)}
+        if "optimize/skipped_steps" in res and self.dist.world > 1:
+            res["optimize/skipped_steps"] *= self.dist.world   # identical on every rank: undo the mean
+        return res
+
+    def histograms(self, out, bins: int = 30) -> Dict[str, Dict]:
+        """The reference's theta histograms (AR.py:218-224: tf.summary.histogram per theta component,
+        exponentiated where the component is a log-parameter, family 'parameters'), over all ranks'
+        samples: min, max, mean, std and `bins` equal-width counts."""
+        theta = out["theta"].detach().float()
+        pos = list(self.mdef.theta_pos) or [False] * theta.shape[1]
+        res = {}
+        for i in range(theta.shape[1]):
+            x = theta[:, i].exp() if pos[i] else theta[:, i]
+            stats = torch.stack([x.min(), -x.max(), x.sum(), (x * x).sum(),
+                                 torch.tensor(float(x.numel()), device=x.device)])
+            if self.dist.world > 1:
+                import torch.distributed as dist
+                mm = stats[:2].clone()
+                dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=self.dist.group)
+                ss = stats[2:].clone()
+                self.dist.all_reduce_(ss)
+                stats = torch.cat([mm, ss])
+            lo, hi, s1, s2, n = stats.double().cpu().tolist()
+            hi = -hi
+            counts = torch.histc(x, bins=bins, min=lo, max=hi if hi > lo else lo + 1.0)
+            self.dist.all_reduce_(counts)
+            mean = s1 / n
+            res[f"parameters/{i}"] = {"min": lo, "max": hi, "mean": mean, "std": max(s2 / n - mean * mean, 0.0) ** 0.5,
+                                      "count": int(n), "edges": [lo, hi], "counts": counts.cpu().tolist()}
+        return res
 
     def train(self, tensorboard_path: Optional[str], save_path: Optional[str], max_runs: Optional[int] = None,
               verbose: bool = True, graph: bool = False):
@@ -260,7 +297,8 @@ class VISSMBase:
                     out = self.elbo_step(self.batch_for(starts), self.global_step)
                 if run % self.log_every == 0:
                     self.last = self.summaries(out)
-                    writer.write(run, self.last)
+                    hist = self.histograms(out)
+                    writer.write(run, self.last, hist)
             self.global_step += 1
             if run == self.early_stopping:
                 converged = True
@@ -275,7 +313,9 @@ class VISSMBase:
 
     # ------------------------------------------------------------------ persistence
     def save(self, PATH: str):
-        """Own checkpoint format: flat params, both Adamax slot sets, step, numpy RNG state."""
+        """Own checkpoint format (torch.save of tensors only, loadable with weights_only=True): flat params,
+        the main and pre-training Adamax slot sets, the global step, the skipped-step count and the numpy
+        global RNG state that draws the windows (AR.py:263-265) -- so a resumed run draws the same windows."""
         d = os.path.dirname(PATH)
         if d:
             os.makedirs(d, exist_ok=True)
@@ -290,6 +330,13 @@ class VISSMBase:
         for i, o in enumerate(self._opt_pre):
             blob[f"pre{i}_v"] = o.v.cpu()
             blob[f"pre{i}_m"] = o.m.cpu()
+        if self._opt_main is not None:
+            blob["skipped_steps"] = self._opt_main.kernel.skipped.cpu()
+        name, key, pos, has_gauss, gauss = np.random.get_state()
+        blob["np_rng_key"] = torch.from_numpy(np.asarray(key, dtype=np.int64))
+        blob["np_rng_meta"] = torch.tensor([int(pos), int(has_gauss)], dtype=torch.int64)
+        blob["np_rng_gauss"] = torch.tensor([float(gauss)], dtype=torch.float64)
+        blob["pre_train"] = torch.tensor(int(bool(self.pre_train)))
         torch.save(blob, PATH)
         print("Model saved")
 
@@ -309,7 +356,13 @@ class VISSMBase:
                 if f"pre{i}_v" in blob:
                     o.v.copy_(blob[f"pre{i}_v"])
                     o.m.copy_(blob[f"pre{i}_m"])
+            if "skipped_steps" in blob:
+                self._opt_main.kernel.skipped.copy_(blob["skipped_steps"])
         self.global_step = int(blob["global_step"])
+        if "np_rng_key" in blob:
+            pos, has_gauss = (int(x) for x in blob["np_rng_meta"].tolist())
+            np.random.set_state(("MT19937", blob["np_rng_key"].numpy().astype(np.uint32), pos, has_gauss,
+                                 float(blob["np_rng_gauss"][0])))
         print("Model restored")
 
     @torch.no_grad()
