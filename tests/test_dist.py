@@ -98,3 +98,58 @@ def test_two_rank_gradient_equals_full_batch():
     assert same
     full = _oracle_grad(_model(), starts, np.arange(P))
     assert np.allclose(reduced, full, rtol=1e-10, atol=1e-10 * np.abs(full).max())
+
+
+def _overlap_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from viforssms_amd.vi_ssm import DistCtx
+    model = _model()
+    model.build_flow()
+    model.dist = DistCtx(rank, world)
+    st = model.store
+    buckets = model._grad_buckets()
+    res = []
+    for overlap in (True, False):
+        model.overlap_allreduce = overlap
+        st.zero_grad()
+        g = torch.Generator().manual_seed(100 + rank)
+        # a loss touching every variable, differently per rank; flows' terms enter in reverse order
+        loss = sum((st[n] * torch.randn(st[n].shape, generator=g, dtype=st[n].dtype)).sum() for n in st.names())
+        model._arm_overlap()
+        loss.backward()
+        launched = len(model._ov["handles"]) if model._ov is not None else 0
+        model._reduce_grads()
+        res.append((launched, st.grad.clone().numpy()))
+    if rank == 0:
+        out.put(([b[0] for b in buckets], res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_overlapped_allreduce_equals_blocking_allreduce():
+    """The per-flow gradient buckets (launched asynchronously from the accumulate hooks during the
+    backward) reduce to exactly the single blocking all-reduce of the flat gradient, on 2 gloo ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    import queue
+    import time
+    deadline = time.time() + 240
+    while True:
+        try:
+            keys, res = q.get(timeout=1)
+            break
+        except queue.Empty:
+            assert not any(p.exitcode not in (None, 0) for p in procs), "a rank failed"
+            assert time.time() < deadline, "timed out"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert keys == ["flow1", "flow0", "rest"]       # backward completion order, q(theta) last
+    (n_ov, g_ov), (n_blk, g_blk) = res
+    assert n_ov == 2 and n_blk == 0                 # both flow buckets went out during the backward
+    assert np.array_equal(g_ov, g_blk)

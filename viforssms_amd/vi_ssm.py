@@ -86,6 +86,8 @@ class VISSMBase:
         # the device (params and slots untouched) and counted in optimize/skipped_steps; False restores the
         # reference's clip_by_global_norm behaviour (NaN written into every variable, AR.py:230-232)
         self.skip_nonfinite = bool(skip_nonfinite)
+        # >1 ranks: all-reduce each flow's gradient bucket as soon as its backward completes (overlap)
+        self.overlap_allreduce = True
         self.T = mdef.scale_num
         self.batch_dims = mdef.M
         self._batch_cache: Dict[tuple, Batch] = {}
@@ -150,6 +152,7 @@ class VISSMBase:
         st.zero_grad()
         out = self.forward(batch, step, eps, x0_theta, row0_dev)
         loss = (-out["elbo"]).sum()
+        self._arm_overlap()
         loss.backward()
         del loss
         # drop the autograd graph now: its parameter-accumulation nodes would otherwise live on into
@@ -177,13 +180,76 @@ class VISSMBase:
         """Optional 0/1 mask over the flat gradient (frozen variables); None = all trainable."""
         return None
 
+    # ------------------------------------------------------------------ gradient all-reduce
+    def _grad_buckets(self):
+        """Per-flow buckets of the flat gradient (each flow's variables are contiguous: flow{i}/...), in the
+        order the backward completes them (last flow first), then the rest (q(theta)'s MAF, complete only
+        at the end).  A flow's bucket is final once every one of its variables has accumulated."""
+        st = self.store
+        groups: Dict[str, List[str]] = {}
+        for n in st.names():
+            key = n.split("/")[0] if n.startswith("flow") else "rest"
+            groups.setdefault(key, []).append(n)
+        out = []
+        for key, names in groups.items():
+            a = st.offsets[names[0]][0]
+            b = st.offsets[names[-1]][0] + st.offsets[names[-1]][1]
+            if b - a != sum(st.offsets[n][1] for n in names):
+                raise RuntimeError(f"gradient bucket {key} is not contiguous")
+            out.append((key, a, b, names))
+        flows = sorted((x for x in out if x[0] != "rest"), key=lambda x: -int(x[0][4:]))
+        return flows + [x for x in out if x[0] == "rest"]
+
+    def _arm_overlap(self):
+        """Before a backward on >1 ranks: each flow bucket's SUM all-reduce is launched (async) from the
+        post-accumulate hook of its last variable, so it runs over xGMI while the earlier flows' backward
+        kernels still execute (LV-cfg's 127 MB gradient); _reduce_grads waits for them."""
+        if (self.dist.world <= 1 or not self.overlap_allreduce
+                or (self.store.grad.is_cuda and torch.cuda.is_current_stream_capturing())):
+            self._ov = None   # (a captured step keeps the single blocking all-reduce)
+            return
+        st = self.store
+        if getattr(self, "_ov_buckets", None) is None:
+            self._ov_buckets = self._grad_buckets()
+            self._ov_owner = {}
+            for bi, (_, a, b, names) in enumerate(self._ov_buckets[:-1]):
+                for n in names:
+                    self._ov_owner[n] = bi
+                    st.tensors[n].register_post_accumulate_grad_hook(self._make_hook(n))
+        self._ov = {"left": [len(x[3]) for x in self._ov_buckets], "handles": {}, "bad": set()}
+
+    def _make_hook(self, name):
+        def hook(t):
+            ov = getattr(self, "_ov", None)
+            if ov is None:
+                return
+            bi = self._ov_owner[name]
+            a, sz = self.store.offsets[name]
+            if t.grad is None or t.grad.data_ptr() != self.store.grad[a:a + sz].data_ptr():
+                ov["bad"].add(bi)   # autograd re-allocated this .grad: reduce the bucket after sync_grads
+            ov["left"][bi] -= 1
+            if ov["left"][bi] == 0 and bi not in ov["bad"]:
+                import torch.distributed as dist
+                _, lo, hi, _ = self._ov_buckets[bi]
+                ov["handles"][bi] = dist.all_reduce(self.store.grad[lo:hi], op=dist.ReduceOp.SUM,
+                                                    group=self.dist.group, async_op=True)
+        return hook
+
     def _reduce_grads(self):
         st = self.store
+        ov, self._ov = getattr(self, "_ov", None), None
         st.sync_grads()
+        if ov is None:
+            self.dist.all_reduce_(st.grad)
+        else:
+            for h in ov["handles"].values():
+                h.wait()
+            for bi, (_, lo, hi, _) in enumerate(self._ov_buckets):
+                if bi not in ov["handles"]:
+                    self.dist.all_reduce_(st.grad[lo:hi])
         m = self.grad_mask()
-        if m is not None:
+        if m is not None:   # elementwise: commutes with the SUM over ranks
             st.grad.mul_(m)
-        self.dist.all_reduce_(st.grad)
 
     def minimize_pair(self, loss1: torch.Tensor, loss2: torch.Tensor, beta1: float = 0.9, lr: float = 1e-3):
         """Two AdamaxOptimizer(lr, beta1).minimize ops run in one session step (gradients from the same
