@@ -1,0 +1,124 @@
+"""LV / SV / FHN log-density kernels (vissm_elbo_fwd / vissm_elbo_bwd, elbo.hip stream_*_kernel<MODEL>)
+against the float64 oracle terms and their autograd:
+  LV  lotka_volterra_partial.py:234-261 + 290-297 (oracle lv_transform / lv_elbo_terms),
+  SV  SV_dense.py:203-223 + 245-246 (sv_elbo_terms on [dim_one; z * mask + shift]),
+  FHN fitz_nag_NVP.py:232-255 (fhn_elbo_terms),
+at window lengths around the kernels' 4-wide chunking (M < 4, M = 4..9, the first interior chunk,
+long odd / even M, the configs' own lengths), one and several windows."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nma_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+MS = [1, 2, 3, 4, 5, 7, 8, 9, 12, 50, 1001, 1508, 2000]
+
+
+def _windows_mask_shift(n_win, D, M, x0, g):
+    """Reference-shaped per-window mask / shift: window 0 pins x_0 (mask 0, shift x0), later windows
+    transform every entry (lotka_volterra_partial.py:381-384, SV_dense.py:322-328)."""
+    mask = torch.ones(n_win, D, M + 1, dtype=torch.float64)
+    shift = torch.zeros(n_win, D, M + 1, dtype=torch.float64)
+    mask[0, :, 0] = 0.0
+    shift[0, :, 0] = torch.as_tensor(x0, dtype=torch.float64)
+    return mask, shift
+
+
+def _case(model, B, M, n_win, seed):
+    g = torch.Generator().manual_seed(seed)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
+    win = torch.randint(0, n_win, (B,), generator=g, dtype=torch.int32)
+    gs, go, ge = r(B), r(B), r(B)
+    d = {"win": win, "gs": gs, "go": go, "ge": ge}
+    if model == "lv":
+        d["z"] = 100 + 10 * r(B, 2 * (M + 1))
+        d["theta"] = torch.stack([math.log(0.5) + 0.1 * r(B), math.log(0.0025) + 0.1 * r(B),
+                                  math.log(0.3) + 0.1 * r(B)], 1)
+        d["mask"], d["shift"] = _windows_mask_shift(n_win, 2, M, [100.0, 100.0], g)
+        d["obs"] = 100 + 10 * r(n_win, 2, M)
+        d["bin"] = (torch.rand(n_win, 2, M, generator=g, dtype=torch.float64) < 0.2).double()
+        d["dt"] = 0.1
+    elif model == "sv":
+        d["z"] = -8 + r(B, M + 1)
+        d["theta"] = torch.stack([0.001 + 0.01 * r(B), -0.6 + 0.1 * r(B), math.log(0.08) + 0.1 * r(B),
+                                  math.log(0.5) + 0.1 * r(B)], 1)
+        m, s = _windows_mask_shift(n_win, 1, M, [-8.5], g)
+        d["mask"], d["shift"] = m[:, 0], s[:, 0]
+        d["dim_one"] = 2 + 14 * torch.rand(n_win, M + 1, generator=g, dtype=torch.float64)
+        d["dt"] = 1.0
+    else:
+        d["z"] = r(B, 2 * (M + 1))
+        d["theta"] = torch.stack([math.log(2) + 0.1 * r(B), 1 + 0.1 * r(B), 1.5 + 0.1 * r(B),
+                                  math.log(0.5) + 0.1 * r(B), math.log(0.3) + 0.1 * r(B)], 1)
+        d["obs"] = r(n_win, 2, M)
+        d["bin"] = (torch.rand(n_win, 2, M, generator=g, dtype=torch.float64) < 0.3).double()
+        d["dt"] = 0.1
+    return d
+
+
+def _oracle(model, d, z, theta):
+    w = d["win"].long()
+    B = z.shape[0]
+    extra = torch.zeros(B, dtype=torch.float64)
+    if model == "lv":
+        x, extra = O.lv_transform(z, d["mask"][w], d["shift"][w])
+        sde, obs = O.lv_elbo_terms(x, theta, d["obs"][w], d["bin"][w], d["dt"])
+    elif model == "sv":
+        x = torch.stack([d["dim_one"][w], z * d["mask"][w] + d["shift"][w]], 1)
+        sde = O.sv_elbo_terms(x, theta, d["dt"])
+        obs = torch.zeros(B, dtype=torch.float64)
+    else:
+        x = z.reshape(B, -1, 2).transpose(1, 2)
+        sde, obs = O.fhn_elbo_terms(x, theta, d["obs"][w], d["bin"][w], d["dt"])
+    return sde, obs, extra
+
+
+@pytest.mark.parametrize("M", MS)
+@pytest.mark.parametrize("n_win", [1, 3])
+@pytest.mark.parametrize("model", ["lv", "sv", "fhn"])
+def test_model_elbo_kernels_match_oracle(model, M, n_win):
+    from viforssms_amd import _lib
+    from viforssms_amd.ops import ElboFeeds, elbo_terms
+    B = 37
+    d = _case(model, B, M, n_win, seed=M * 13 + n_win + len(model))
+    zr, thr = d["z"].clone().requires_grad_(True), d["theta"].clone().requires_grad_(True)
+    sde_r, obs_r, ex_r = _oracle(model, d, zr, thr)
+    loss = (sde_r * d["gs"]).sum()
+    if model != "sv":
+        loss = loss + (obs_r * d["go"]).sum()
+    if model == "lv":
+        loss = loss + (ex_r * d["ge"]).sum()
+    loss.backward()
+
+    f = lambda k: d[k].float().to(DEV).contiguous() if k in d else None
+    feeds = ElboFeeds(obs=f("obs"), obs_bin=f("bin"), mask=f("mask"), shift=f("shift"), dim_one=f("dim_one"),
+                      win=d["win"].to(DEV) if n_win > 1 else None, n_win=n_win)
+    mid = {"lv": _lib.MODEL_LV, "sv": _lib.MODEL_SV, "fhn": _lib.MODEL_FHN}[model]
+    zd = d["z"].float().to(DEV).requires_grad_(True)
+    thd = d["theta"].float().to(DEV).requires_grad_(True)
+    sde, obs, ex = elbo_terms(mid, M, d["dt"], 1.0, feeds, zd, thd)
+    dl = (sde * f("gs")).sum()
+    if model != "sv":
+        dl = dl + (obs * f("go")).sum()
+    if model == "lv":
+        dl = dl + (ex * f("ge")).sum()
+    dl.backward()
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        return float((a - b).norm() / (b.norm() + 1e-30))
+
+    tol = 2e-5
+    assert rel(sde, sde_r) < tol
+    if model != "sv":
+        assert rel(obs, obs_r) < tol
+    if model == "lv":
+        assert rel(ex, ex_r) < tol
+    assert torch.isfinite(zd.grad).all()
+    assert rel(zd.grad, zr.grad) < 1e-4
+    assert rel(thd.grad, thr.grad) < 1e-4

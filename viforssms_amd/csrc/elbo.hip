@@ -1,8 +1,7 @@
-// ELBO log-density kernels: one 256-thread block per trajectory (LV, SV, FHN) or one
-// wave per trajectory (AR, the streaming path below), fixed-order block / wave
-// reductions (double accumulation).  Streaming: the path z is read once
-// (forward) or once plus its neighbours (backward, which recomputes each
-// transition from both of its endpoints instead of exchanging partials).
+// ELBO log-density kernels, all streaming with one wave per trajectory: the path z is read
+// once with 16-byte loads (the backward also writes dz with 16-byte stores), the per-window
+// feeds are L2-resident, per-sample constants are hoisted and the per-sample sums are fixed-order
+// wave reductions in double (no block barriers).
 //
 // Reference terms: AR VI_SSM._ELBO (AR.py:168-187); LV Softplus transform and
 // _ELBO (lotka_volterra_partial.py:290-297, 234-270); SV dim-one concat and
@@ -19,204 +18,538 @@ struct Args {
   VissmElboData d;
 };
 
+// ---------------------------------------------------------------------------
+// LV / SV / FHN streaming path: one wave per trajectory (kSW per 256-thread block), each lane owning
+// chunks of kV = 4 consecutive times; a chunk's stored z (LV / FHN: 2 kV interleaved floats, SV: kV)
+// and its per-window feed rows (mask / shift / dim_one / obs / obs_bin, L2-resident) are read with
+// 16-byte loads, kSU chunks in flight per lane.  The forward evaluates the chunk's kV transitions
+// t0 -> t0+1 .. (its states plus the next one); the backward evaluates the kV + 1 transitions touching
+// its elements once each (states t0-1 .. t0+kV) and writes the chunk's dz with 16-byte stores.
+// Per-lane partials in fp32 over a few dozen chunks, wave reductions in double (fixed order, no
+// block barrier).  The first chunk and the tail (t < kV, t >= kV floor(M/kV)) take a per-element path.
+// ---------------------------------------------------------------------------
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+constexpr int kV = 4;   // times per chunk
+constexpr int kSU = 2;  // chunks per lane in flight
+constexpr int kSW = 4;  // trajectories (waves) per 256-thread block
+
+__device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
+
+// N consecutive floats from p (16-byte loads, then an 8-byte and a 4-byte load for the rest)
+template <int N>
+__device__ __forceinline__ void ldn(const float* __restrict__ p, float (&o)[N]) {
+#pragma unroll
+  for (int i = 0; i + 4 <= N; i += 4) {
+    const f4u v = ld4(p + i);
+    o[i] = v[0]; o[i + 1] = v[1]; o[i + 2] = v[2]; o[i + 3] = v[3];
+  }
+  constexpr int r = N / 4 * 4;
+  if constexpr (N - r >= 2) {
+    const f2u v = *reinterpret_cast<const f2u*>(p + r);
+    o[r] = v[0]; o[r + 1] = v[1];
+  }
+  if constexpr ((N - r) % 2 == 1) o[N - 1] = p[N - 1];
+}
+
+struct St {
+  float x[2];  // state
+  float j[2];  // d state / d stored z
+};
+
 template <int MODEL>
-struct Model;
+struct Dev;
 
-// x at time t for dimension d and its derivative w.r.t. the stored z entry
-template <>
-struct Model<VISSM_MODEL_AR> {
-  static constexpr int D = 1, P = 3;
-  __device__ static float x(const Args&, const float* zb, int, int t, int, float* dxdz) {
-    *dxdz = 1.f;
-    return zb[t];
-  }
-  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float) {
-    return em::ar_trans(xh[0], xt[0], th);
-  }
-  __device__ static int zidx(int t, int) { return t; }
-};
+// fast transcendentals for the streaming path: hardware exp / log / rcp (v_exp_f32, v_log_f32, v_rcp_f32:
+// ~1 ulp), with the small-argument branches that keep log1p / expm1 accurate
+// (no denormal range scaling: the arguments here are far from the denormal range, and an
+// underflowing e^x flushing to 0 is the right limit)
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float flog(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// log1p(e) for e in [0, 1]
+__device__ __forceinline__ float flog1p01(float e) { return e > 1e-3f ? flog(1.f + e) : e * (1.f - 0.5f * e); }
+// 1 - e^{-y} for y > 0 (= -expm1(-y)); the libm path only where a lane needs it (small y)
+__device__ __forceinline__ float one_minus_exp_neg(float y) {
+  return y > 0.25f ? 1.f - fexp(-y) : -::expm1f(-y);
+}
 
+// LV: x = softplus(z) * mask + shift per coordinate (lotka_volterra_partial.py:290-297), obs N(., 1),
+// log q += Softplus ILDJ at x_{t+1}; the Cholesky EM density with exp(theta) hoisted per sample
 template <>
-struct Model<VISSM_MODEL_LV> {
-  static constexpr int D = 2, P = 3;
-  __device__ static float x(const Args& a, const float* zb, int w, int t, int d, float* dxdz) {
-    const float zz = zb[2 * t + d];
-    const size_t mi = (static_cast<size_t>(w) * 2 + d) * (a.M + 1) + t;
-    const float mk = a.d.mask[mi];
-    *dxdz = mk * em::sigmoid_h(zz);
-    return em::softplus_h(zz) * mk + a.d.shift[mi];
+struct Dev<VISSM_MODEL_LV> {
+  static constexpr int P = 3, ZD = 2, SU = 1;  // (registers: one chunk in flight per lane)
+  static constexpr bool kObs = true, kExtra = true;
+  static constexpr float kSd = 1.f;
+  float e0, e1, e2, dt, idt, c_lp;
+  int M;
+  const float *mk, *sh, *ob, *bn;  // window rows: mask / shift [2][M+1], obs / obs_bin [2][M]
+  __device__ void init(const Args& a, const float* thp, int w) {
+    e0 = ::expf(thp[0]); e1 = ::expf(thp[1]); e2 = ::expf(thp[2]);
+    dt = a.dt;
+    idt = 1.f / dt;
+    c_lp = -::logf(dt) - em::kLog2Pi_;   // -1/2 log(dt^2) - log 2 pi
+    M = a.M;
+    mk = a.d.mask + static_cast<size_t>(w) * 2 * (M + 1);
+    sh = a.d.shift + static_cast<size_t>(w) * 2 * (M + 1);
+    ob = a.d.obs + static_cast<size_t>(w) * 2 * M;
+    bn = a.d.obs_bin + static_cast<size_t>(w) * 2 * M;
   }
-  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
-    return em::lv_trans(xh, xt, th, dt);
+  // softplus and its derivative from one exp: e = e^{-|z|}, softplus = max(z, 0) + log1p(e)
+  __device__ static void tf(float zz, float m, float s, float* x, float* j) {
+    const float e = fexp(-::fabsf(zz));
+    *x = (::fmaxf(zz, 0.f) + flog1p01(e)) * m + s;
+    const float r = frcp(1.f + e);
+    *j = m * (zz >= 0.f ? r : e * r);
   }
-  __device__ static int zidx(int t, int d) { return 2 * t + d; }
-};
-
-template <>
-struct Model<VISSM_MODEL_SV> {
-  static constexpr int D = 2, P = 4;
-  __device__ static float x(const Args& a, const float* zb, int w, int t, int d, float* dxdz) {
-    const size_t mi = static_cast<size_t>(w) * (a.M + 1) + t;
-    if (d == 0) {
-      *dxdz = 0.f;
-      return a.d.dim_one[mi];
+  template <int N>
+  __device__ void states(const float* zb, int t0, St (&o)[N]) const {
+    float zz[2 * N], m0[N], m1[N], s0[N], s1[N];
+    ldn<2 * N>(zb + 2 * t0, zz);
+    ldn<N>(mk + t0, m0);
+    ldn<N>(mk + (M + 1) + t0, m1);
+    ldn<N>(sh + t0, s0);
+    ldn<N>(sh + (M + 1) + t0, s1);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      tf(zz[2 * i], m0[i], s0[i], &o[i].x[0], &o[i].j[0]);
+      tf(zz[2 * i + 1], m1[i], s1[i], &o[i].x[1], &o[i].j[1]);
     }
-    const float mk = a.d.mask[mi];
-    *dxdz = mk;
-    return zb[t] * mk + a.d.shift[mi];
   }
-  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
-    return em::sv_trans(xh, xt, th, dt);
+  __device__ St state(const float* zb, int t) const {
+    St o;
+    tf(zb[2 * t], mk[t], sh[t], &o.x[0], &o.j[0]);
+    tf(zb[2 * t + 1], mk[M + 1 + t], sh[M + 1 + t], &o.x[1], &o.j[1]);
+    return o;
   }
-  __device__ static int zidx(int t, int) { return t; }
+  // em::lv_trans with the exponentials hoisted, det / dt^2 = e0 x1 (Bv + e2 x2) + Bv e2 x2 (a sum of
+  // positive terms: no cancellation) and one reciprocal
+  __device__ em::TG trans(const St& p, const St& q) const {
+    em::TG r;
+    const float x1 = p.x[0], x2 = p.x[1];
+    const float p12 = x1 * x2;
+    const float Bv = e1 * p12, a1 = e0 * x1, c2 = e2 * x2;
+    const float A = a1 + Bv, Cc = Bv + c2;
+    const float m1 = dt * (a1 - Bv), m2 = dt * (Bv - c2);
+    const float q1 = q.x[0] - x1 - m1, q2 = q.x[1] - x2 - m2;
+    const float Dl = a1 * Cc + Bv * c2;
+    const float iD = frcp(Dl), inv = iD * idt;
+    const float g1 = inv * (Cc * q1 + Bv * q2), g2 = inv * (Bv * q1 + A * q2);
+    const float quad = q1 * g1 + q2 * g2;
+    r.lp = -0.5f * flog(Dl) - 0.5f * quad + c_lp;
+    const float gq1 = -g1, gq2 = -g2;
+    float gA = -0.5f * Cc * iD - 0.5f * (q2 * q2 * inv - quad * Cc * iD);
+    float gC = -0.5f * A * iD - 0.5f * (q1 * q1 * inv - quad * A * iD);
+    float gB = Bv * iD - q1 * q2 * inv - quad * Bv * iD;
+    r.gt[0] = gq1;
+    r.gt[1] = gq2;
+    float gx1 = -gq1, gx2 = -gq2;
+    const float gm1 = -gq1, gm2 = -gq2;
+    float ge0 = gm1 * dt * x1, ge1 = 0.f, ge2 = -gm2 * dt * x2;
+    gx1 += gm1 * dt * e0;
+    gx2 += -gm2 * dt * e2;
+    gB += (gm2 - gm1) * dt;
+    gB += gC;
+    ge2 += gC * x2;
+    gx2 += gC * e2;
+    ge0 += gA * x1;
+    gx1 += gA * e0;
+    gB += gA;
+    ge1 += gB * p12;
+    const float gp = gB * e1;
+    gx1 += gp * x2;
+    gx2 += gp * x1;
+    r.gh[0] = gx1;
+    r.gh[1] = gx2;
+    r.gth[0] = ge0 * e0;
+    r.gth[1] = ge1 * e1;
+    r.gth[2] = ge2 * e2;
+    r.gth[3] = r.gth[4] = 0.f;
+    return r;
+  }
+  // Softplus ILDJ at y: -log(1 - e^{-y}), derivative -e^{-y} / (1 - e^{-y}) = 1 - 1 / (1 - e^{-y})
+  __device__ static float ildj(float y, float* g) {
+    const float v = one_minus_exp_neg(y);
+    *g = 1.f - frcp(v);
+    return -flog(v);
+  }
 };
 
+// SV: state (dim_one, z * mask + shift) (SV_dense.py:245-246), no obs term
 template <>
-struct Model<VISSM_MODEL_FHN> {
-  static constexpr int D = 2, P = 5;
-  __device__ static float x(const Args&, const float* zb, int, int t, int d, float* dxdz) {
-    *dxdz = 1.f;
-    return zb[2 * t + d];
+struct Dev<VISSM_MODEL_SV> {
+  static constexpr int P = 4, ZD = 1, SU = kSU;
+  static constexpr bool kObs = false, kExtra = false;
+  static constexpr float kSd = 1.f;
+  float th[4], dt, sq, e2, s2, is2, c_lp;
+  int M;
+  const float *mk, *sh, *d1, *ob, *bn;
+  __device__ void init(const Args& a, const float* thp, int w) {
+    th[0] = thp[0]; th[1] = thp[1]; th[2] = thp[2]; th[3] = thp[3];
+    dt = a.dt;
+    sq = ::sqrtf(dt);
+    e2 = ::expf(th[2]);
+    s2 = sq * ::expf(th[3]);
+    is2 = 1.f / s2;
+    // -log sqrt(dt) (of s1) - log s2 - log 2 pi
+    c_lp = -::logf(sq) - ::logf(s2) - em::kLog2Pi_;
+    M = a.M;
+    mk = a.d.mask + static_cast<size_t>(w) * (M + 1);
+    sh = a.d.shift + static_cast<size_t>(w) * (M + 1);
+    d1 = a.d.dim_one + static_cast<size_t>(w) * (M + 1);
+    ob = bn = nullptr;
   }
-  __device__ static em::TG trans(const float* xh, const float* xt, const float* th, float dt) {
-    return em::fhn_trans(xh, xt, th, dt);
+  template <int N>
+  __device__ void states(const float* zb, int t0, St (&o)[N]) const {
+    float zz[N], m[N], s[N], x1[N];
+    ldn<N>(zb + t0, zz);
+    ldn<N>(mk + t0, m);
+    ldn<N>(sh + t0, s);
+    ldn<N>(d1 + t0, x1);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      o[i].x[0] = x1[i];
+      o[i].j[0] = 0.f;
+      o[i].x[1] = zz[i] * m[i] + s[i];
+      o[i].j[1] = m[i];
+    }
   }
-  __device__ static int zidx(int t, int d) { return 2 * t + d; }
+  __device__ St state(const float* zb, int t) const {
+    St o;
+    o.x[0] = d1[t];
+    o.j[0] = 0.f;
+    o.x[1] = zb[t] * mk[t] + sh[t];
+    o.j[1] = mk[t];
+    return o;
+  }
+  // em::sv_trans with the per-sample terms hoisted and one reciprocal:
+  //   s1 = sqrt(dt) x1 e^{x2/2},  log|s1| = log sqrt(dt) + log|x1| + x2 / 2
+  __device__ em::TG trans(const St& p, const St& q) const {
+    em::TG r;
+    const float x1 = p.x[0], x2 = p.x[1];
+    const float ex = fexp(0.5f * x2);
+    const float s1 = sq * x1 * ex, is1 = frcp(s1);
+    const float m1 = dt * th[0] * x1, m2 = dt * (th[1] - e2 * x2);
+    const float q1 = q.x[0] - x1 - m1, q2 = q.x[1] - x2 - m2;
+    const float z1 = q1 * is1, z2 = q2 * is2;
+    r.lp = -0.5f * (z1 * z1 + z2 * z2) - (flog(::fabsf(x1)) + 0.5f * x2) + c_lp;
+    const float gq1 = -z1 * is1, gq2 = -z2 * is2;
+    const float gs1 = (z1 * z1 - 1.f) * is1, gs2 = (z2 * z2 - 1.f) * is2;
+    r.gt[0] = gq1;
+    r.gt[1] = gq2;
+    float gx1 = -gq1, gx2 = -gq2;
+    const float gm1 = -gq1, gm2 = -gq2;
+    r.gth[0] = gm1 * dt * x1;
+    gx1 += gm1 * dt * th[0];
+    r.gth[1] = gm2 * dt;
+    r.gth[2] = -gm2 * dt * x2 * e2;
+    gx2 += -gm2 * dt * e2;
+    gx1 += gs1 * sq * ex;
+    gx2 += gs1 * 0.5f * s1;
+    r.gth[3] = gs2 * s2;
+    r.gth[4] = 0.f;
+    r.gh[0] = gx1;
+    r.gh[1] = gx2;
+    return r;
+  }
+  __device__ static float ildj(float, float* g) { *g = 0.f; return 0.f; }
 };
 
-// number of stored z entries per sample
-template <int MODEL>
-__device__ __forceinline__ int zlen(const Args& a) {
-  return (MODEL == VISSM_MODEL_LV || MODEL == VISSM_MODEL_FHN) ? 2 * (a.M + 1) : (a.M + 1);
-}
+// FHN: x = z (interleaved), obs N(., 0.1) (fitz_nag_NVP.py:232-234)
+template <>
+struct Dev<VISSM_MODEL_FHN> {
+  static constexpr int P = 5, ZD = 2, SU = kSU;
+  static constexpr bool kObs = true, kExtra = false;
+  static constexpr float kSd = 0.1f;
+  float th[5], dt, E0, is1, is2, c_lp;
+  int M;
+  const float *ob, *bn;
+  __device__ void init(const Args& a, const float* thp, int w) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) th[i] = thp[i];
+    dt = a.dt;
+    E0 = ::expf(th[0]);
+    const float sq = ::sqrtf(dt), s1 = sq * ::sqrtf(::expf(th[3])), s2 = sq * ::sqrtf(::expf(th[4]));
+    is1 = 1.f / s1;
+    is2 = 1.f / s2;
+    c_lp = -::logf(s1) - ::logf(s2) - em::kLog2Pi_;
+    M = a.M;
+    ob = a.d.obs + static_cast<size_t>(w) * 2 * M;
+    bn = a.d.obs_bin + static_cast<size_t>(w) * 2 * M;
+  }
+  template <int N>
+  __device__ void states(const float* zb, int t0, St (&o)[N]) const {
+    float zz[2 * N];
+    ldn<2 * N>(zb + 2 * t0, zz);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      o[i].x[0] = zz[2 * i];
+      o[i].x[1] = zz[2 * i + 1];
+      o[i].j[0] = o[i].j[1] = 1.f;
+    }
+  }
+  __device__ St state(const float* zb, int t) const {
+    St o;
+    o.x[0] = zb[2 * t];
+    o.x[1] = zb[2 * t + 1];
+    o.j[0] = o.j[1] = 1.f;
+    return o;
+  }
+  // em::fhn_trans with the per-sample scales hoisted (s_i = sqrt(dt e^{th_{3,4}}), their reciprocals
+  // and logs): no division per transition
+  __device__ em::TG trans(const St& p, const St& q) const {
+    em::TG r;
+    const float x1 = p.x[0], x2 = p.x[1];
+    const float f = x1 - x1 * x1 * x1 - x2 + th[1];
+    const float m1 = dt * E0 * f, m2 = dt * (th[2] * x1 - x2 + 1.4f);
+    const float q1 = q.x[0] - x1 - m1, q2 = q.x[1] - x2 - m2;
+    const float z1 = q1 * is1, z2 = q2 * is2;
+    r.lp = -0.5f * (z1 * z1 + z2 * z2) + c_lp;
+    const float gq1 = -z1 * is1, gq2 = -z2 * is2;
+    r.gt[0] = gq1;
+    r.gt[1] = gq2;
+    float gx1 = -gq1, gx2 = -gq2;
+    const float gm1 = -gq1, gm2 = -gq2;
+    r.gth[0] = gm1 * dt * E0 * f;
+    const float gf = gm1 * dt * E0;
+    gx1 += gf * (1.f - 3.f * x1 * x1);
+    gx2 += -gf;
+    r.gth[1] = gf;
+    r.gth[2] = gm2 * dt * x1;
+    gx1 += gm2 * dt * th[2];
+    gx2 += -gm2 * dt;
+    r.gth[3] = 0.5f * (z1 * z1 - 1.f);   // gs1 s1 / 2 with gs1 = (z1^2 - 1) / s1
+    r.gth[4] = 0.5f * (z2 * z2 - 1.f);
+    r.gh[0] = gx1;
+    r.gh[1] = gx2;
+    return r;
+  }
+  __device__ static float ildj(float, float* g) { *g = 0.f; return 0.f; }
+};
 
 template <int MODEL>
-__device__ __forceinline__ float obs_sd(const Args& a) {
-  return MODEL == VISSM_MODEL_AR ? a.obs_std : (MODEL == VISSM_MODEL_FHN ? 0.1f : 1.f);
-}
-template <int MODEL>
-__device__ __forceinline__ constexpr bool has_obs() { return MODEL != VISSM_MODEL_SV; }
-
-template <int MODEL>
-__global__ __launch_bounds__(256) void elbo_fwd_kernel(Args a, const float* __restrict__ z,
-                                                       const float* __restrict__ theta, float* __restrict__ sde,
-                                                       float* __restrict__ obs, float* __restrict__ extra) {
-  using Mdl = Model<MODEL>;
-  constexpr int D = Mdl::D, P = Mdl::P;
-  __shared__ double red[4];
-  const int b = blockIdx.x;
+__global__ __launch_bounds__(256) void stream_fwd_kernel(Args a, const float* __restrict__ z,
+                                                         const float* __restrict__ theta, float* __restrict__ sde,
+                                                         float* __restrict__ obs, float* __restrict__ extra) {
+  using Dv = Dev<MODEL>;
+  constexpr int ZD = Dv::ZD, P = Dv::P;
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kSW + (threadIdx.x >> 6));
+  if (b >= a.B) return;  // wave-uniform
+  const int M = a.M;
   const int w = a.d.win ? a.d.win[b] : 0;
-  const float* zb = z + static_cast<size_t>(b) * zlen<MODEL>(a);
-  float th[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < P; ++i) th[i] = theta[static_cast<size_t>(b) * P + i];
-  const float osd = obs_sd<MODEL>(a);
-  double s_sde = 0.0, s_obs = 0.0, s_ex = 0.0;
-  for (int t = threadIdx.x; t < a.M; t += blockDim.x) {
-    float xh[2], xt[2], dd;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      xh[d] = Mdl::x(a, zb, w, t, d, &dd);
-      xt[d] = Mdl::x(a, zb, w, t + 1, d, &dd);
+  Dv m;
+  m.init(a, theta + static_cast<size_t>(b) * P, w);
+  const float* zb = z + static_cast<size_t>(b) * ZD * (M + 1);
+  const float isd = 1.f / Dv::kSd;
+  float s_lp = 0.f, s_q = 0.f, s_b = 0.f, s_e = 0.f;
+  // transition t: x_t -> x_{t+1}; the obs of row t and the ILDJ observe x_{t+1}
+  auto tr = [&](const St& p, const St& q, float y0, float y1, float b0, float b1) {
+    s_lp += m.trans(p, q).lp;
+    if constexpr (Dv::kObs) {
+      const float z0 = (q.x[0] - y0) * isd, z1 = (q.x[1] - y1) * isd;
+      s_q += b0 * z0 * z0 + b1 * z1 * z1;
+      s_b += b0 + b1;
     }
-    s_sde += Mdl::trans(xh, xt, th, a.dt).lp;
-    if (has_obs<MODEL>()) {
+    if constexpr (Dv::kExtra) {
+      float g;
+      s_e += Dv::ildj(q.x[0], &g) + Dv::ildj(q.x[1], &g);
+    }
+  };
+  const int nfull = M / kV;  // chunks whose kV transitions all exist
+  int c = lane;
+  constexpr int SU = Dv::SU;
+  for (; c + 64 * (SU - 1) < nfull; c += 64 * SU) {
+    St st[SU][kV + 1];
+    float y[SU][2][kV], bb[SU][2][kV];
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const size_t oi = (static_cast<size_t>(w) * D + d) * a.M + t;
-        float gx;
-        s_obs += em::obs_term(xt[d], a.d.obs[oi], a.d.obs_bin[oi], osd, &gx);
+    for (int u = 0; u < SU; ++u) {
+      const int t0 = kV * (c + 64 * u);
+      m.template states<kV + 1>(zb, t0, st[u]);
+      if constexpr (Dv::kObs) {
+        ldn<kV>(m.ob + t0, y[u][0]);
+        ldn<kV>(m.ob + M + t0, y[u][1]);
+        ldn<kV>(m.bn + t0, bb[u][0]);
+        ldn<kV>(m.bn + M + t0, bb[u][1]);
       }
     }
-    if (MODEL == VISSM_MODEL_LV) {
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        float gy;
-        s_ex += em::sp_ildj(xt[d], &gy);
-      }
+    for (int u = 0; u < SU; ++u)
+#pragma unroll
+      for (int j = 0; j < kV; ++j)
+        tr(st[u][j], st[u][j + 1], Dv::kObs ? y[u][0][j] : 0.f, Dv::kObs ? y[u][1][j] : 0.f,
+           Dv::kObs ? bb[u][0][j] : 0.f, Dv::kObs ? bb[u][1][j] : 0.f);
+  }
+  for (; c < nfull; c += 64) {
+    const int t0 = kV * c;
+    St st[kV + 1];
+    m.template states<kV + 1>(zb, t0, st);
+#pragma unroll
+    for (int j = 0; j < kV; ++j) {
+      const int t = t0 + j;
+      tr(st[j], st[j + 1], Dv::kObs ? m.ob[t] : 0.f, Dv::kObs ? m.ob[M + t] : 0.f, Dv::kObs ? m.bn[t] : 0.f,
+         Dv::kObs ? m.bn[M + t] : 0.f);
     }
   }
-  const double r0 = block_sum(s_sde, red);
-  const double r1 = block_sum(s_obs, red);
-  const double r2 = block_sum(s_ex, red);
-  if (threadIdx.x == 0) {
-    sde[b] = static_cast<float>(r0);
-    if (obs) obs[b] = static_cast<float>(r1);
-    if (extra) extra[b] = static_cast<float>(r2);
+  for (int t = kV * nfull + lane; t < M; t += 64)
+    tr(m.state(zb, t), m.state(zb, t + 1), Dv::kObs ? m.ob[t] : 0.f, Dv::kObs ? m.ob[M + t] : 0.f,
+       Dv::kObs ? m.bn[t] : 0.f, Dv::kObs ? m.bn[M + t] : 0.f);
+  const double r_lp = wave_sum(static_cast<double>(s_lp));
+  const double r_q = wave_sum(static_cast<double>(s_q));
+  const double r_b = wave_sum(static_cast<double>(s_b));
+  const double r_e = wave_sum(static_cast<double>(s_e));
+  if (lane == 0) {
+    sde[b] = static_cast<float>(r_lp);
+    if (obs) obs[b] = Dv::kObs ? static_cast<float>(-0.5 * r_q + r_b * (-std::log(static_cast<double>(Dv::kSd)) -
+                                                                     0.5 * kLog2Pi))
+                               : 0.f;
+    if (extra) extra[b] = static_cast<float>(r_e);
   }
 }
 
+// d/dz of gs sde + go obs + ge extra at every stored z entry, d/dtheta of gs sde.  Element e takes the
+// head gradient of transition e (e < M) and, for e >= 1, the tail gradient of transition e - 1 and the
+// obs / ILDJ terms observing x_e.
 template <int MODEL>
-__global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __restrict__ z,
-                                                       const float* __restrict__ theta,
-                                                       const float* __restrict__ g_sde,
-                                                       const float* __restrict__ g_obs,
-                                                       const float* __restrict__ g_ex, float* __restrict__ dz,
-                                                       float* __restrict__ dtheta) {
-  using Mdl = Model<MODEL>;
-  constexpr int D = Mdl::D, P = Mdl::P;
-  __shared__ double red[4];
-  const int b = blockIdx.x;
+__global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __restrict__ z,
+                                                         const float* __restrict__ theta,
+                                                         const float* __restrict__ g_sde,
+                                                         const float* __restrict__ g_obs,
+                                                         const float* __restrict__ g_ex, float* __restrict__ dz,
+                                                         float* __restrict__ dtheta) {
+  using Dv = Dev<MODEL>;
+  constexpr int ZD = Dv::ZD, P = Dv::P;
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kSW + (threadIdx.x >> 6));
+  if (b >= a.B) return;  // wave-uniform
+  const int M = a.M;
   const int w = a.d.win ? a.d.win[b] : 0;
-  const float* zb = z + static_cast<size_t>(b) * zlen<MODEL>(a);
-  float* dzb = dz + static_cast<size_t>(b) * zlen<MODEL>(a);
-  float th[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < P; ++i) th[i] = theta[static_cast<size_t>(b) * P + i];
+  Dv m;
+  m.init(a, theta + static_cast<size_t>(b) * P, w);
+  const float* zb = z + static_cast<size_t>(b) * ZD * (M + 1);
+  float* dzb = dz + static_cast<size_t>(b) * ZD * (M + 1);
   const float gs = g_sde ? g_sde[b] : 0.f;
-  const float go = (has_obs<MODEL>() && g_obs) ? g_obs[b] : 0.f;
-  const float ge = (MODEL == VISSM_MODEL_LV && g_ex) ? g_ex[b] : 0.f;
-  const float osd = obs_sd<MODEL>(a);
-  double acc[5] = {0, 0, 0, 0, 0};
-  for (int t = threadIdx.x; t <= a.M; t += blockDim.x) {
-    float xc[2], jac[2], xo[2], dd;
+  const float go = (Dv::kObs && g_obs) ? g_obs[b] : 0.f;
+  const float ge = (Dv::kExtra && g_ex) ? g_ex[b] : 0.f;
+  const float cgo = -go / (Dv::kSd * Dv::kSd);
+  float acc[P];
 #pragma unroll
-    for (int d = 0; d < D; ++d) xc[d] = Mdl::x(a, zb, w, t, d, &jac[d]);
-    float gx[2] = {0.f, 0.f};
-    if (t < a.M) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) xo[d] = Mdl::x(a, zb, w, t + 1, d, &dd);
-      const em::TG r = Mdl::trans(xc, xo, th, a.dt);
-#pragma unroll
-      for (int d = 0; d < D; ++d) gx[d] += gs * r.gh[d];
-#pragma unroll
-      for (int i = 0; i < P; ++i) acc[i] += static_cast<double>(gs) * r.gth[i];
+  for (int i = 0; i < P; ++i) acc[i] = 0.f;
+  // the gradient w.r.t. x_e of the terms observing x_e (obs row e - 1, ILDJ), e >= 1
+  auto obs_g = [&](const St& s, float y0, float y1, float b0, float b1, float* g) {
+    if constexpr (Dv::kObs) {
+      g[0] += cgo * b0 * (s.x[0] - y0);
+      g[1] += cgo * b1 * (s.x[1] - y1);
     }
-    if (t >= 1) {
+    if constexpr (Dv::kExtra) {
+      float d0, d1;
+      Dv::ildj(s.x[0], &d0);
+      Dv::ildj(s.x[1], &d1);
+      g[0] += ge * d0;
+      g[1] += ge * d1;
+    }
+  };
+  auto head = [&](const em::TG& r, float* g) {
+    g[0] += gs * r.gh[0];
+    g[1] += gs * r.gh[1];
 #pragma unroll
-      for (int d = 0; d < D; ++d) xo[d] = Mdl::x(a, zb, w, t - 1, d, &dd);
-      const em::TG r = Mdl::trans(xo, xc, th, a.dt);
+    for (int i = 0; i < P; ++i) acc[i] += r.gth[i];
+  };
+  auto tail = [&](const em::TG& r, float* g) {
+    g[0] += gs * r.gt[0];
+    g[1] += gs * r.gt[1];
+  };
+  // interior chunks c in [1, M / kV): t0 >= 1 and t0 + kV <= M, states t0-1 .. t0+kV exist
+  const int ihi = M / kV;
+  int c = 1 + lane;
+  auto chunk = [&](int t0, const St (&st)[kV + 2], const float (&y)[2][kV], const float (&bb)[2][kV]) {
+    // transitions t0-1 .. t0+kV-1 in order, each evaluated once: element t0 + j = st[j + 1] takes the
+    // tail of the previous one and the head of the next
+    em::TG prev = m.trans(st[0], st[1]);
+    float o[ZD * kV];
 #pragma unroll
-      for (int d = 0; d < D; ++d) gx[d] += gs * r.gt[d];
-      if (has_obs<MODEL>()) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          const size_t oi = (static_cast<size_t>(w) * D + d) * a.M + (t - 1);
-          float g;
-          em::obs_term(xc[d], a.d.obs[oi], a.d.obs_bin[oi], osd, &g);
-          gx[d] += go * g;
-        }
-      }
-      if (MODEL == VISSM_MODEL_LV) {
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          float g;
-          em::sp_ildj(xc[d], &g);
-          gx[d] += ge * g;
-        }
+    for (int j = 0; j < kV; ++j) {
+      const em::TG cur = m.trans(st[j + 1], st[j + 2]);
+      float g[2] = {0.f, 0.f};
+      head(cur, g);
+      tail(prev, g);
+      prev = cur;
+      obs_g(st[j + 1], y[0][j], y[1][j], bb[0][j], bb[1][j], g);
+      if constexpr (ZD == 2) {
+        o[2 * j] = g[0] * st[j + 1].j[0];
+        o[2 * j + 1] = g[1] * st[j + 1].j[1];
+      } else {
+        o[j] = g[1] * st[j + 1].j[1];
       }
     }
-    if (MODEL == VISSM_MODEL_SV) {
-      dzb[t] = gx[1] * jac[1];
+#pragma unroll
+    for (int i = 0; i < ZD * kV; i += 4)
+      *reinterpret_cast<f4u*>(dzb + ZD * t0 + i) = f4u{o[i], o[i + 1], o[i + 2], o[i + 3]};
+  };
+  constexpr int SU = Dv::SU;
+  for (; c + 64 * (SU - 1) < ihi; c += 64 * SU) {
+    St st[SU][kV + 2];
+    float y[SU][2][kV], bb[SU][2][kV];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int t0 = kV * (c + 64 * u);
+      m.template states<kV + 2>(zb, t0 - 1, st[u]);
+      if constexpr (Dv::kObs) {  // rows t0-1 .. t0+kV-2 observe x_{t0} .. x_{t0+kV-1}
+        ldn<kV>(m.ob + t0 - 1, y[u][0]);
+        ldn<kV>(m.ob + M + t0 - 1, y[u][1]);
+        ldn<kV>(m.bn + t0 - 1, bb[u][0]);
+        ldn<kV>(m.bn + M + t0 - 1, bb[u][1]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kV; ++j) y[u][0][j] = y[u][1][j] = bb[u][0][j] = bb[u][1][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) chunk(kV * (c + 64 * u), st[u], y[u], bb[u]);
+  }
+  for (; c < ihi; c += 64) {
+    const int t0 = kV * c;
+    St st[kV + 2];
+    float y[2][kV], bb[2][kV];
+    m.template states<kV + 2>(zb, t0 - 1, st);
+    if constexpr (Dv::kObs) {
+      ldn<kV>(m.ob + t0 - 1, y[0]);
+      ldn<kV>(m.ob + M + t0 - 1, y[1]);
+      ldn<kV>(m.bn + t0 - 1, bb[0]);
+      ldn<kV>(m.bn + M + t0 - 1, bb[1]);
     } else {
 #pragma unroll
-      for (int d = 0; d < D; ++d) dzb[Mdl::zidx(t, d)] = gx[d] * jac[d];
+      for (int j = 0; j < kV; ++j) y[0][j] = y[1][j] = bb[0][j] = bb[1][j] = 0.f;
+    }
+    chunk(t0, st, y, bb);
+  }
+  // the rest, one element per lane: t in [0, kV) and [kV ihi, M]
+  const int lo_end = ihi >= 1 ? kV : M + 1;  // with no interior chunk the first range covers everything
+  const int nrest = lo_end + (ihi >= 1 ? (M + 1 - kV * ihi) : 0);
+  for (int r = lane; r < nrest; r += 64) {
+    const int t = r < lo_end ? r : kV * ihi + (r - lo_end);
+    if (t > M || (r >= lo_end && t < lo_end)) continue;
+    const St sc = m.state(zb, t);
+    float g[2] = {0.f, 0.f};
+    if (t < M) head(m.trans(sc, m.state(zb, t + 1)), g);
+    if (t >= 1) {
+      tail(m.trans(m.state(zb, t - 1), sc), g);
+      if constexpr (Dv::kObs)
+        obs_g(sc, m.ob[t - 1], m.ob[M + t - 1], m.bn[t - 1], m.bn[M + t - 1], g);
+      else
+        obs_g(sc, 0.f, 0.f, 0.f, 0.f, g);
+    }
+    if constexpr (ZD == 2) {
+      dzb[2 * t] = g[0] * sc.j[0];
+      dzb[2 * t + 1] = g[1] * sc.j[1];
+    } else {
+      dzb[t] = g[1] * sc.j[1];
     }
   }
 #pragma unroll
   for (int i = 0; i < P; ++i) {
-    const double s = block_sum(acc[i], red);
-    if (threadIdx.x == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(s);
+    const double s = wave_sum(static_cast<double>(acc[i]));
+    if (lane == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(gs * s);
   }
 }
 
@@ -233,7 +566,6 @@ __global__ __launch_bounds__(256) void elbo_bwd_kernel(Args a, const float* __re
 // reductions in double (fixed order, no block barrier), and each lane keeps kArU chunks of
 // loads in flight.  Per-lane partials are fp32 over at most a few dozen chunks.
 // ---------------------------------------------------------------------------
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 constexpr int kArV = 4;  // consecutive times per chunk (one 16-byte load)
 #ifndef VISSM_AR_U
 #define VISSM_AR_U 8
@@ -244,7 +576,6 @@ constexpr int kArV = 4;  // consecutive times per chunk (one 16-byte load)
 constexpr int kArU = VISSM_AR_U;  // chunks per lane in flight
 constexpr int kArW = 4;           // trajectories (waves) per 256-thread block
 
-__device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 __device__ __forceinline__ f4u ldz4(const float* p) {
   if constexpr (VISSM_AR_NT) return __builtin_nontemporal_load(reinterpret_cast<const f4u*>(p));
   return ld4(p);
@@ -460,13 +791,13 @@ int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   if (d->B == 0) return VISSM_OK;
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
-  dim3 grid(d->B), blk(256);
+  dim3 grid((d->B + kSW - 1) / kSW), blk(256);
   prof_begin(VISSM_PROF_ELBO_FWD, st);
   switch (d->model) {
     case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_fwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, sde, obs); break;
-    case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
-    case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
-    default: hipLaunchKernelGGL(elbo_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    case VISSM_MODEL_LV: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
+    default: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
   }
   VISSM_CHECK_LAUNCH("elbo_fwd");
   // algorithmic bytes: z read once, theta read, the per-sample sums written (per-window feeds are
@@ -484,13 +815,13 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   if (d->B == 0) return VISSM_OK;
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
-  dim3 grid(d->B), blk(256);
+  dim3 grid((d->B + kSW - 1) / kSW), blk(256);
   prof_begin(VISSM_PROF_ELBO_BWD, st);
   switch (d->model) {
     case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
-    case VISSM_MODEL_LV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
-    case VISSM_MODEL_SV: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
-    default: hipLaunchKernelGGL(elbo_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    case VISSM_MODEL_LV: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
+    default: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
   }
   VISSM_CHECK_LAUNCH("elbo_bwd");
   // algorithmic bytes: z read, dz written, theta / dtheta and the upstream gradients
