@@ -2,9 +2,16 @@
 torch tensors.  The update is the reference's Adamax without bias correction:
     v <- beta1 v + (1 - beta1) g ;  m <- max(beta2 m + eps, |g|) ;  var <- var - lr v / m
 with eps = 1e-8 (1e-7 for fp16 variables), slots "v" (first moment) and "m" (inf-norm) starting
-at zero.  apply_gradients runs one fused HIP kernel per variable (or one over the whole flat
-buffer when the variables are views of a viforssms_amd ParamStore, as VI_SSM does);
-clip_norm reproduces tf.clip_by_global_norm inside the same kernel.
+at zero.
+
+apply_gradients runs ONE fused HIP launch pair (vissm_adamax_step: fixed-order global norm, then the
+update) over a flat fp32 image of every variable of a dtype: the variables' slots live in one flat
+buffer per dtype (get_slot returns views of it); gradients and values are packed into flat buffers,
+updated, and written back -- or updated in place when the variables already are consecutive views
+of one buffer (a viforssms_amd ParamStore, as VI_SSM's are).  Variables of any layout (non-contiguous
+views included) and fp16 variables (updated in fp32, rounded back) are accepted.  clip_norm > 0 is
+tf.clip_by_global_norm over all the variables: fused into the kernel for one dtype group, a device
+scale from vissm_sqnorm otherwise (no host synchronisation either way).
 """
 from __future__ import annotations
 
@@ -12,7 +19,45 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
-from .ops import AdamaxKernel
+from .ops import AdamaxKernel, sqnorm
+
+
+class _Group:
+    """The variables of one dtype / device in one apply_gradients call: flat slots and a kernel."""
+
+    def __init__(self, vars_: List[torch.Tensor]):
+        self.vars = vars_
+        self.sizes = [v.numel() for v in vars_]
+        n = sum(self.sizes)
+        dev = vars_[0].device
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.kernel = AdamaxKernel(n, dev)
+        self.eps = 1e-7 if vars_[0].dtype == torch.float16 else 1e-8
+        self.flat_view = self._consecutive_view()
+
+    def _consecutive_view(self) -> Optional[torch.Tensor]:
+        """A flat fp32 view covering every variable when they are contiguous, in order and adjacent in one
+        storage (then the update runs in place); None otherwise."""
+        v0 = self.vars[0]
+        if v0.dtype != torch.float32:
+            return None
+        ptr = v0.data_ptr()
+        st = v0.untyped_storage().data_ptr()
+        for v, sz in zip(self.vars, self.sizes):
+            if not v.is_contiguous() or v.data_ptr() != ptr or v.untyped_storage().data_ptr() != st:
+                return None
+            ptr += 4 * sz
+        base = v0.detach()
+        return torch.as_strided(base, (sum(self.sizes),), (1,), base.storage_offset())
+
+    def slot_views(self, name: str) -> List[torch.Tensor]:
+        buf = self.v if name == "v" else self.m
+        out, a = [], 0
+        for var, sz in zip(self.vars, self.sizes):
+            out.append(buf[a:a + sz].view(var.shape))
+            a += sz
+        return out
 
 
 class AdamaxOptimizer:
@@ -21,18 +66,21 @@ class AdamaxOptimizer:
         self._beta1 = beta1
         self._beta2 = beta2
         self._name = name
-        self._slots: Dict[int, Dict[str, torch.Tensor]] = {}
-        self._kernels: Dict[int, AdamaxKernel] = {}
+        self._groups: Dict[tuple, _Group] = {}
+        self._slot_of: Dict[int, Dict[str, torch.Tensor]] = {}
 
     # -- slots --------------------------------------------------------------------------
-    def _create_slots(self, var_list):
-        for v in var_list:
-            if id(v) not in self._slots:
-                self._slots[id(v)] = {"m": torch.zeros_like(v, memory_format=torch.contiguous_format),
-                                      "v": torch.zeros_like(v, memory_format=torch.contiguous_format)}
+    def _group_for(self, vars_: List[torch.Tensor]) -> _Group:
+        key = tuple(id(v) for v in vars_)
+        g = self._groups.get(key)
+        if g is None:
+            g = self._groups[key] = _Group(vars_)
+            for var, sv, sm in zip(vars_, g.slot_views("v"), g.slot_views("m")):
+                self._slot_of[id(var)] = {"v": sv, "m": sm}
+        return g
 
     def get_slot(self, var, name):
-        return self._slots.get(id(var), {}).get(name)
+        return self._slot_of.get(id(var), {}).get(name)
 
     def get_slot_names(self):
         return ["m", "v"]
@@ -53,24 +101,34 @@ class AdamaxOptimizer:
         pairs = [(g, v) for g, v in grads_and_vars if g is not None]
         if not pairs:
             raise ValueError("No gradients provided for any variable")
-        self._create_slots([v for _, v in pairs])
-        if clip_norm and clip_norm > 0:
-            # one global norm across all variables: scale the gradients once, then update unclipped
-            gn = torch.sqrt(sum((g.float() ** 2).sum() for g, _ in pairs))
-            scale = clip_norm * torch.minimum(1.0 / gn, torch.tensor(1.0 / clip_norm, device=gn.device))
-            if not torch.isfinite(gn):
-                scale = torch.tensor(float("nan"), device=gn.device)
-            pairs = [(g * scale, v) for g, v in pairs]
+        by: Dict[tuple, List[Tuple[torch.Tensor, torch.Tensor]]] = {}
+        for g, v in pairs:
+            if v.dtype not in (torch.float32, torch.float16):
+                raise TypeError(f"Adamax: unsupported variable dtype {v.dtype}")
+            by.setdefault((v.dtype, v.device), []).append((g, v))
+        clip = float(clip_norm) if clip_norm and clip_norm > 0 else 0.0
         with torch.no_grad():
-            for g, v in pairs:
-                s = self._slots[id(v)]
-                eps = 1e-7 if v.dtype == torch.float16 else 1e-8
-                k = self._kernels.get(v.numel())
-                if k is None:
-                    k = self._kernels[v.numel()] = AdamaxKernel(v.numel(), v.device)
-                target = v.detach()
-                k.step(target.view(-1), g.detach().contiguous().view(-1), s["v"].view(-1), s["m"].view(-1),
-                       self._lr, self._beta1, self._beta2, eps, 0.0)
+            flat_g = {k: torch.cat([g.detach().reshape(-1).float() for g, _ in ps]) for k, ps in by.items()}
+            if clip > 0 and len(by) > 1:
+                # one global norm across the dtype groups: the clip scale on the device, applied up front
+                sq = sum(sqnorm(fg) for fg in flat_g.values())
+                gn = torch.sqrt(sq)
+                scale = torch.where(torch.isfinite(gn), clip * torch.minimum(1.0 / gn, torch.full_like(gn, 1.0 / clip)),
+                                    torch.full_like(gn, float("nan")))
+                flat_g = {k: fg * scale for k, fg in flat_g.items()}
+                clip = 0.0
+            for k, ps in by.items():
+                grp = self._group_for([v for _, v in ps])
+                P = grp.flat_view
+                inplace = P is not None
+                if not inplace:
+                    P = torch.cat([v.detach().reshape(-1).float() for _, v in ps])
+                grp.kernel.step(P, flat_g[k], grp.v, grp.m, self._lr, self._beta1, self._beta2, grp.eps, clip)
+                if not inplace:
+                    a = 0
+                    for (_, v), sz in zip(ps, grp.sizes):
+                        v.copy_(P[a:a + sz].view(v.shape))
+                        a += sz
         if global_step is not None and torch.is_tensor(global_step):
             global_step.add_(1)
 
