@@ -217,6 +217,8 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured HIP graph (viforssms_amd.graph; needs warmup >= 3)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--fuse", choices=["on", "off"], default="on",
+                    help="AR at bf16 / bf16x3: run the last flow fused with the ELBO terms (vissm_flow_ar_elbo_fused)")
     ap.add_argument("--parity-line", choices=["auto", "off"], default="auto",
                     help="also time the step at bf16x3 (AR, bf16, 1 GPU) and report it as parity_precision")
     ap.add_argument("--cpu-B", type=int, default=64)
@@ -241,6 +243,7 @@ def main():
     prec = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}[args.precision]
 
     model, meta = build_model(args, ctx, dev, prec)
+    model.engine.fuse_last = args.fuse == "on"
     lib = _lib.load()
 
     def step(i):
@@ -335,7 +338,8 @@ def main():
         "dtype": args.precision,
         "data": meta["data"],
         "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": args.T,
-                   "parallelism": f"dp{world}", "hip_graph": bool(args.graph)},
+                   "parallelism": f"dp{world}", "hip_graph": bool(args.graph),
+                   "last_flow_fused": bool(model.engine.fused_ok(model.batch_for(model.select_windows()), B))},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                      "kernel": kernel, "flops_per_launch": flops_per_launch,

@@ -131,6 +131,29 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w,
                    void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * The last flow of the AR(1) stack fused with its ELBO terms: forward AND backward of
+ * IAF._create_flow / IAF.slp (AR.py:50-89) for the final flow together with VI_SSM._ELBO's
+ * AR(1) transition and observation terms (AR.py:168-176), for the loss
+ *     loss = -scale * sum_b (sde_b + obs_b + logsig_b)        (scale = T / M, AR.py:184)
+ * i.e. the part of -sum_b ELBO_b (AR.py:228-229) that depends on this flow.  The kernel
+ * recomputes the flow's output x = u_next itself and evaluates the gradient of the AR(1) terms
+ * on the fly, so vissm_flow_fwd for this flow and the ELBO backward's dz are not needed.  theta is
+ * the per-sample AR(1) theta [B][3], obs / obs_bin the per-window feeds [n_win][M] (M = L - k - 1).
+ * Writes x [B][M+1] (the latent path; the caller takes sde / obs and their theta gradient from it
+ * with vissm_elbo_fwd / vissm_elbo_bwd), logsig [B] (the n_logsig counted outputs), du [B][L],
+ * dC [n_win][Lh][H], dtheta_term [B][H] and the weight gradients of the loss.
+ * Supported: bf16 / bf16x3, one hidden layer, no BN, stride 1, k <= 32. */
+int32_t vissm_flow_ar_elbo_fused_supported(const VissmFlowDesc* d);
+size_t vissm_flow_ar_elbo_fused_workspace_size(const VissmFlowDesc* d);
+int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w,
+                             const float* u, const float* C, const int32_t* win,
+                             const float* theta_term, const float* theta,
+                             const float* obs, const float* obs_bin, float obs_std,
+                             float scale, float* x, float* logsig, float* du,
+                             float* dC, float* dtheta_term, const VissmFlowGrads* g,
+                             void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * ELBO log-densities over a path, one model per id:
  *   AR  : VI_SSM._ELBO obs + AR(1) terms (AR.py:168-176)
  *   LV  : softplus transform + ILDJ (lotka_volterra_partial.py:290-297),
@@ -167,7 +190,8 @@ int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data,
                    const float* z, const float* theta, float* sde, float* obs,
                    float* extra, void* stream);
 
-/* dLoss/d(sde, obs, extra) per sample -> dz [B][D*(M+1)], dtheta [B][P_theta]. */
+/* dLoss/d(sde, obs, extra) per sample -> dz [B][D*(M+1)], dtheta [B][P_theta].  dz may be NULL
+ * (only dtheta wanted, e.g. after vissm_flow_ar_elbo_fused, which differentiates through x itself). */
 int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data,
                    const float* z, const float* theta, const float* g_sde,
                    const float* g_obs, const float* g_extra, float* dz,

@@ -188,7 +188,10 @@ def oracle_reference(model, batch, eps: torch.Tensor, x0: torch.Tensor):
 def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
                     device: str = "cuda:0", T: Optional[int] = None, starts=None, precision: int = 0,
                     seed: int = 3, impute: Optional[int] = None, condition: bool = False,
-                    fp32_yardstick: bool = False) -> Dict:
+                    fp32_yardstick: bool = False, step_path: bool = False) -> Dict:
+    """step_path: the product side runs the training step's gradient (VI_SSM.elbo_step without the
+    Adamax apply: for AR at bf16 / bf16x3 the last flow fused with the ELBO terms) instead of
+    forward + autograd backward."""
     torch.cuda.set_device(torch.device(device))
     model = build_model(family, B, M, k, n_flows, H, n_layers, fw, device, T=T, precision=precision, seed=seed,
                         impute=impute, condition=condition)
@@ -203,10 +206,14 @@ def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n
 
     # ---- product (GPU) ----
     st = model.store
-    st.zero_grad()
-    out = model.forward(batch, 0, eps=eps.float().to(device).contiguous(), x0_theta=x0.float().to(device))
-    loss = (-out["elbo"]).sum()
-    loss.backward()
+    if step_path:
+        out = model.elbo_step(batch, 0, eps=eps.float().to(device).contiguous(), x0_theta=x0.float().to(device),
+                              apply=False)
+    else:
+        st.zero_grad()
+        out = model.forward(batch, 0, eps=eps.float().to(device).contiguous(), x0_theta=x0.float().to(device))
+        loss = (-out["elbo"]).sum()
+        loss.backward()
     st.sync_grads()
     torch.cuda.synchronize()
     elbo_gpu = out["elbo"].detach().double().cpu().numpy()
@@ -229,6 +236,7 @@ def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n
         r, q = ref_g[n], grads_gpu[n]
         per[n] = float(np.linalg.norm(q - r) / (np.linalg.norm(r) + 1e-6 * gnorm + 1e-30))
     return {
+        "fused": bool(step_path and model.engine.fused_ok(batch, B)),
         "elbo_rel_err": elbo_err,
         "grad_rel_err": float(np.linalg.norm(ggpu - gref) / (gnorm + 1e-30)),
         "grad_max_param_err": max(per.values()),

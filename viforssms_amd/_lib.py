@@ -67,6 +67,12 @@ SIGNATURES = {
     "vissm_flow_bwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                               ctypes.POINTER(FlowGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_flow_ar_elbo_fused_supported": (_i32, [ctypes.POINTER(FlowDesc)]),
+    "vissm_flow_ar_elbo_fused_workspace_size": (_size_t, [ctypes.POINTER(FlowDesc)]),
+    "vissm_flow_ar_elbo_fused": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _f32,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        ctypes.POINTER(FlowGrads), _c_void_p, _size_t, _c_void_p]),
     "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,

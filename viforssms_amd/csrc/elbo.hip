@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
     }
 #pragma unroll
     for (int i = 0; i < ZD * kV; i += 4)
-      *reinterpret_cast<f4u*>(dzb + ZD * t0 + i) = f4u{o[i], o[i + 1], o[i + 2], o[i + 3]};
+      if (dz) *reinterpret_cast<f4u*>(dzb + ZD * t0 + i) = f4u{o[i], o[i + 1], o[i + 2], o[i + 3]};
   };
   constexpr int SU = Dv::SU;
   for (; c + 64 * (SU - 1) < ihi; c += 64 * SU) {
@@ -539,6 +539,7 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
       else
         obs_g(sc, 0.f, 0.f, 0.f, 0.f, g);
     }
+    if (!dz) continue;
     if constexpr (ZD == 2) {
       dzb[2 * t] = g[0] * sc.j[0];
       dzb[2 * t + 1] = g[1] * sc.j[1];
@@ -695,7 +696,7 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
       a1 += zt * xs[j + 1];
       a2 += zt * zt - 1.f;
     }
-    *reinterpret_cast<f4u*>(dzb + t0) = g;
+    if (dz) *reinterpret_cast<f4u*>(dzb + t0) = g;
   };
   const int ilo = 1, ihi = M / kArV;  // chunks i in [ilo, ihi), kArU per lane at a time
   int i = ilo + lane;
@@ -726,7 +727,8 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
     const float xc = zb[t];
     const float xp = t >= 1 ? zb[t - 1] : 0.f, xn = t < M ? zb[t + 1] : 0.f;
     const float y = t >= 1 ? yb[t - 1] : 0.f, bn = t >= 1 ? bb[t - 1] : 0.f;
-    dzb[t] = elem(t, xp, xc, xn, y, bn);
+    const float gv = elem(t, xp, xc, xn, y, bn);
+    if (dz) dzb[t] = gv;
   }
   // dlp/dth0 = sum z/s, dlp/dth1 = sum z x_t / s, dlp/dth2 = sum (z^2 - 1)
   const double r0 = wave_sum(static_cast<double>(a0));
@@ -811,7 +813,7 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
                    void* stream) {
   int rc = check(d, data);
   if (rc) return rc;
-  VISSM_CHECK_ARG(z && theta && dz && dtheta, "elbo_bwd: null pointer");
+  VISSM_CHECK_ARG(z && theta && dtheta, "elbo_bwd: null pointer");
   if (d->B == 0) return VISSM_OK;
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
@@ -826,7 +828,7 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   VISSM_CHECK_LAUNCH("elbo_bwd");
   // algorithmic bytes: z read, dz written, theta / dtheta and the upstream gradients
   prof_end(VISSM_PROF_ELBO_BWD, st,
-           4.0 * d->B * (2.0 * zlen_of(d) + 2 * theta_len(d->model) + 3));
+           4.0 * d->B * ((dz ? 2.0 : 1.0) * zlen_of(d) + 2 * theta_len(d->model) + 3));
   return VISSM_OK;
 }
 

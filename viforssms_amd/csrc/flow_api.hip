@@ -26,6 +26,13 @@ int flow5_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 int flow5_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 
+bool flow5_ar_fused_supports(const VissmFlowDesc* d);
+size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d);
+int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+                   const float* theta_term, const float* theta, const float* obs, const float* obs_bin, float obs_std,
+                   float scale, float* x, float* logsig, float* du, float* dC, float* dtheta_term,
+                   const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st);
+
 static bool use_flow4(const VissmFlowDesc* d) { return d->n_hidden <= 1; }
 
 static int validate(const VissmFlowDesc* d) {
@@ -96,6 +103,33 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   if (use_flow4(d))
     return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
   return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
+}
+
+int32_t vissm_flow_ar_elbo_fused_supported(const VissmFlowDesc* d) {
+  return (validate(d) == VISSM_OK && flow5_ar_fused_supports(d)) ? 1 : 0;
+}
+
+size_t vissm_flow_ar_elbo_fused_workspace_size(const VissmFlowDesc* d) {
+  if (!vissm_flow_ar_elbo_fused_supported(d)) return 0;
+  return flow5_ar_fused_workspace_size(d);
+}
+
+int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+                             const int32_t* win, const float* theta_term, const float* theta, const float* obs,
+                             const float* obs_bin, float obs_std, float scale, float* x, float* logsig,
+                             float* du, float* dC, float* dtheta_term, const VissmFlowGrads* gr, void* workspace,
+                             size_t ws_bytes, void* stream) {
+  int rc = validate(d);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(flow5_ar_fused_supports(d),
+                  "flow_ar_elbo_fused: needs bf16 / bf16x3, one hidden layer, no BN, stride 1, k <= 32");
+  VISSM_CHECK_ARG(w && u && C && theta_term && theta && obs && obs_bin && x && logsig && du && dC && dtheta_term && gr,
+                  "flow_ar_elbo_fused: null pointer");
+  VISSM_CHECK_ARG(gr->w_eps && gr->w_hid && gr->b_hid && gr->w_head && gr->b_head, "flow_ar_elbo_fused: null grad");
+  VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_ar_elbo_fused: n_win > 1 needs win[]");
+  VISSM_CHECK_ARG(obs_std > 0.f, "flow_ar_elbo_fused: obs_std must be positive");
+  return flow5_ar_fused(d, w, u, C, win, theta_term, theta, obs, obs_bin, obs_std, scale, x, logsig, du, dC,
+                        dtheta_term, gr, workspace, ws_bytes, as_stream(stream));
 }
 
 }  // extern "C"

@@ -208,6 +208,36 @@ struct KArgs {
   int dcb;  // backward: the block's waves share a chunk and sum their dC tiles (one window)
 };
 
+// The last flow of the AR(1) stack fused with its ELBO terms (vissm_flow_ar_elbo_fused): the backward
+// kernel recomputes the flow's output x = u_next itself, so it evaluates the gradient of the AR(1)
+// transition and observation terms on the fly instead of reading an upstream gradient; the flow's
+// forward launch is not needed.  Loss part: -scale sum_b (sde_b + obs_b + logsig_b) (AR.py:168-185).
+// A tile computes 16 columns but produces the gradients of 15 positions: column 15 is the next
+// position's x (the head of the transition out of position 14); x at the previous tile's last position
+// rides in a per-sample carry, and a chunk other than the first starts one tile early (outputs
+// discarded) to obtain it.  The kernel writes x (for the per-sample sde / obs / d theta sums, which a
+// streaming kernel takes afterwards) and per-column log sigma partial sums (fixed order: tiles, then
+// the 16 columns at the item's end) to a [n_chunks][B] slab.
+struct FzArgs {
+  const float* theta;  // [B][3] AR(1) theta per sample
+  const float* obs;    // [n_win][M] observations y_t (pairs with x_{t+1})
+  const float* bin;    // [n_win][M] observation mask
+  float* x;            // [B][M + 1] the flow's output (the latent path)
+  float* lsl;          // [n_chunks][B] log sigma partial sums
+  float scale;         // T / M
+  float iosd;          // 1 / obs_std
+  int M;               // transitions (x has M + 1 entries = the flow's Lout)
+};
+// x of the neighbouring column within a 16-lane row (DPP row shifts: no LDS)
+__device__ __forceinline__ float row_prev(float v) {  // lane c <- lane c - 1 (c = 0 keeps v)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0x111, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_next(float v) {  // lane c <- lane c + 1 (c = 15 keeps v)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0x101, 0xf, 0xf, false));
+}
+
 // backward dC tiles summed over a block's NW groups before the slab (one window only): the dC
 // slab per AR-cfg launch 4.1 -> 1.0 GB and its reduce 0.74 -> 0.19 ms, but the tile barriers'
 // wave skew costs the kernel 0.8 ms: measured 126.9 vs 125.8 ms per AR-cfg step, so off
@@ -373,6 +403,19 @@ __device__ __forceinline__ void fence_fwd() {
 #ifndef VISSM_BWD_FENCES
 #define VISSM_BWD_FENCES 0xff
 #endif
+#ifndef VISSM_LANE_SCALARS
+#define VISSM_LANE_SCALARS 1  // per-sample window index / d log q read once per item into lane b, then
+                              // v_readlane per unit (no scalar load + lgkmcnt(0) drain per unit)
+#endif
+#ifndef VISSM_BWD_WHP
+#define VISSM_BWD_WHP 1  // head-backward A fragments: all four LDS reads issued unconditionally up front
+                         // (a masked read per MFMA serialised four LDS round trips)
+#endif
+// value of lane `bl` of v (bl wave-uniform)
+__device__ __forceinline__ int lane_i(int v, int bl) { return __builtin_amdgcn_readlane(v, bl); }
+__device__ __forceinline__ float lane_f(float v, int bl) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), bl));
+}
 template <int BIT>
 __device__ __forceinline__ void fence_bwd() {
   if constexpr ((VISSM_BWD_FENCES >> BIT) & 1) fence();
@@ -623,11 +666,12 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   constexpr bool REGW = false;
   const FwdRegs<NH, KB, NP> wr{};
 #endif
+  const int lwi = (VISSM_LANE_SCALARS && win && lane < nb) ? win[b_lo + lane] : 0;
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     const float* ub = u + static_cast<size_t>(b) * a.L;
     float* ob = u_next + static_cast<size_t>(b) * a.Lout;
-    const int wi = win ? win[b] : 0;
+    const int wi = VISSM_LANE_SCALARS ? lane_i(lwi, bl) : (win ? win[b] : 0);
     const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
     float ls = 0.f;
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
@@ -662,14 +706,16 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
 // ---------------------------------------------------------------------------
 // backward kernel: one work item per wave; tiles outer, samples inner
 // ---------------------------------------------------------------------------
-template <int NH, int KB, int JB, int NP>
+template <int NH, int KB, int JB, int NP, bool FZ = false>
 __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const float* __restrict__ gout, const float* __restrict__ dls,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ du, float* __restrict__ dC_slab,
                                                     float* __restrict__ dth_slab, float* __restrict__ dW_slab,
-                                                    float* __restrict__ halo) {
+                                                    float* __restrict__ halo, FzArgs fz = FzArgs{}) {
+  static_assert(!FZ || NH == 1, "the fused AR(1) ELBO variant has one hidden layer");
+  constexpr int PO = FZ ? P - 1 : P;  // output positions per tile (FZ: column 15 is look-ahead only)
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
   constexpr int NS = NH + 1;   // images: I_0 .. I_NH (reused for dZ_l and dA0)
@@ -688,7 +734,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   constexpr bool PADDED = JB <= 2;
   constexpr int QW = PADDED ? 2 * P + KP : P;
   __shared__ float dscr[NW][KP][QW];
+  __shared__ float zls[FZ ? NW : 1][FZ ? S : 1][P];  // FZ: per-sample, per-column log sigma sums over the tiles
+  __shared__ float zcar[FZ ? NW : 1][FZ ? S : 1];     // FZ: x at the previous tile's last position
   load_shared(sh, img, cst);
+  if constexpr (FZ) {
+    for (int i = threadIdx.x; i < NW * S * P; i += NT) (&zls[0][0][0])[i] = 0.f;
+    for (int i = threadIdx.x; i < NW * S; i += NT) (&zcar[0][0])[i] = 0.f;
+  }
   for (int i = threadIdx.x; i < NW * S * DTH; i += NT) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW * S * KP; i += NT) (&carry[0][0][0])[i] = 0.f;
   if constexpr (PADDED)
@@ -745,23 +797,44 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   const bf4 ones4 = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
   const int fwc = 16 * NH + 4 * KB, fis = 16 * NH + 4 * KB + 2 * JB + 2;
 
-  for (int m0 = m_lo; m0 < m_hi; m0 += P) {
-    const int nP = min(P, m_hi - m0), t0 = a.s * m0, fin = a.s * nP;
+  const int lwi = (VISSM_LANE_SCALARS && win && lane < nb) ? win[b_lo + lane] : 0;
+  const float ldl = (!FZ && VISSM_LANE_SCALARS && lane < nb) ? dls[b_lo + lane] : 0.f;
+  float lt0 = 0.f, lt1 = 0.f, lis = 0.f;  // FZ: theta_0, theta_1, e^{-theta_2} of sample b_lo + lane
+  if constexpr (FZ) {
+    if (lane < nb) {
+      const float* tp = fz.theta + static_cast<size_t>(b_lo + lane) * 3;
+      lt0 = tp[0];
+      lt1 = tp[1];
+      lis = __expf(-tp[2]);
+    }
+  }
+  // FZ: a chunk after the first starts one tile early; that tile only provides x at position m_lo - 1
+  const int m_start = (FZ && chn > 0) ? m_lo - PO : m_lo;
+  for (int m0 = m_start; m0 < m_hi; m0 += PO) {
+    const bool discard = FZ && m0 < m_lo;  // wave-uniform
+    const int nP = discard ? 0 : min(PO, m_hi - m0), t0 = a.s * m0, fin = a.s * nP;
+    const int nZ = FZ ? min(P, a.Lh - m0) : nP;  // columns with real inputs
     f4 dCa[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
     for (int bl = 0; bl < nb; ++bl) {
       fence_bwd<0>();
       const int b = b_lo + bl;
-      const int wi = win ? win[b] : 0;
+      const int wi = VISSM_LANE_SCALARS ? lane_i(lwi, bl) : (win ? win[b] : 0);
       const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
-      const float dl = dls[b];
+      const float dl = FZ ? -fz.scale : (VISSM_LANE_SCALARS ? lane_f(ldl, bl) : dls[b]);
       f4 XN[4];
       float mu, rr;
+      float fz_yp = 0.f, fz_bp = 0.f;  // FZ: the observation of x_t (row t - 1), loaded with the unit's inputs
       {
+        if constexpr (FZ) {
+          const size_t wo = static_cast<size_t>(wi) * fz.M + min(max(m0 + c - 1, 0), fz.M - 1);
+          fz_yp = fz.obs[wo];
+          fz_bp = fz.bin[wo];
+        }
         Win<KB> wn;
-        fetch_win<KB>(a, u + static_cast<size_t>(b) * a.L, gout + static_cast<size_t>(b) * a.Lout, t0, wn);
-        load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, XN);
+        fetch_win<KB>(a, u + static_cast<size_t>(b) * a.L, FZ ? nullptr : gout + static_cast<size_t>(b) * a.Lout, t0, wn);
+        load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nZ, XN);
         stage_win<KB>(wn, uw, gw);
       }
       u2 i0p[4];
@@ -773,7 +846,40 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       const int oq = a.s * c + (a.s - 1);
       const bool pv = c < nP;
       const float sig = softplus_fast(rr) + 1e-10f;
-      const float gmu = pv ? gw[oq] : 0.f;
+      float gmu;
+      if constexpr (FZ) {
+        // x at t = m0 + c (column c < nZ), its neighbours from the adjacent columns / the carry
+        const float x = uw[c + a.k] * sig + mu;
+        float xp = row_prev(x);
+        const float xn = row_next(x);
+        if (c == 0) xp = zcar[w][bl];
+        if (discard) {
+          if (lane == PO - 1) zcar[w][bl] = x;
+          continue;
+        }
+        const float th0 = lane_f(lt0, bl), th1 = lane_f(lt1, bl), is = lane_f(lis, bl);
+        const int t = m0 + c;
+        // branch-free: every lane loads (clamped indices) and masks with 0 / 1 factors
+        const float fh = (pv && t < fz.M) ? 1.f : 0.f;  // transition t: x_t -> x_{t+1}
+        const float ft = (pv && t >= 1) ? 1.f : 0.f;    // transition t - 1 and its observation of x_t
+        const float yp = fz_yp, bp = fz_bp * ft;
+        const float zt = fh * (xn - th1 * x - th0) * is;
+        const float zp = ft * (x - th1 * xp - th0) * is;
+        // d(sde + obs)/dx_t
+        const float de = th1 * zt * is - zp * is - bp * (x - yp) * (fz.iosd * fz.iosd);
+        gmu = -fz.scale * de;  // 0 for columns without an output
+        const float lsg = (t0 + oq >= a.Lout - a.n_logsig) ? __logf(sig) : 0.f;
+        if (g == 0) {
+          gw[c] = gmu;  // the upstream-gradient window the rest of the unit reads
+          if (pv) {
+            fz.x[static_cast<size_t>(b) * (fz.M + 1) + t] = x;
+            zls[w][bl][c] += lsg;
+          }
+        }
+        if (lane == PO - 1 && nP == PO) zcar[w][bl] = x;
+      } else {
+        gmu = pv ? gw[oq] : 0.f;
+      }
       float dsig = gmu * uw[oq + a.k];
       if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * __frcp_rn(sig);
       const float gr = dsig * sigmoid_fast(rr);
@@ -830,11 +936,24 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       {
         const bool g0 = g == 0;
         const Fr4<NP> gf2 = split4<NP>(f4{g0 ? gmu : 0.f, g0 ? gr : 0.f, 0.f, 0.f});
+        unsigned wvh[4], wvl[4];
+        if constexpr (VISSM_BWD_WHP) {
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            wvh[rb] = whp[16 * rb + c];
+            if constexpr (NP == 3) wvl[rb] = whp[HP + 16 * rb + c];
+          }
+        }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           Fr4<NP> wa;
-          wa.h = __builtin_bit_cast(bf4, u2{g0 ? whp[16 * rb + c] : 0u, 0u});
-          if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? whp[HP + 16 * rb + c] : 0u, 0u});
+          if constexpr (VISSM_BWD_WHP) {
+            wa.h = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
+            if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u});
+          } else {
+            wa.h = __builtin_bit_cast(bf4, u2{g0 ? whp[16 * rb + c] : 0u, 0u});
+            if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? whp[HP + 16 * rb + c] : 0u, 0u});
+          }
           D[rb] = mm<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? D[rb][r] * elu_d(XN[rb][r]) : 0.f;
@@ -1039,6 +1158,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   }
 
   if (!valid) return;
+  if constexpr (FZ) {
+    if (lane < nb) {  // lane bl: its sample's columns in order
+      float v = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < P; ++cc) v += zls[w][lane][cc];
+      fz.lsl[static_cast<size_t>(chn) * a.B + b_lo + lane] = v;
+    }
+  }
   // ---- per-sample tails: carry -> halo / du tail; d theta -> slab ----
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
@@ -1103,15 +1230,15 @@ struct Geom {
   int blocks;     // grid size
 };
 
-static Geom geom(const VissmFlowDesc* d, bool backward) {
+static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   Geom g;
   g.s = d->stride2 ? 2 : 1;
   g.Lout = d->L - d->k;
   g.Lh = g.Lout / g.s;
   g.S = (backward && d->n_win > 1) ? 1 : S;
   g.n_groups = (d->B + g.S - 1) / g.S;
-  g.n_tiles = (g.Lh + P - 1) / P;
-  int ch_min_tiles = ((d->k + g.s - 1) / g.s + P - 1) / P;
+  g.n_tiles = (g.Lh + po - 1) / po;
+  int ch_min_tiles = ((d->k + g.s - 1) / g.s + po - 1) / po;
   if (ch_min_tiles < 1) ch_min_tiles = 1;
   const int target_items = 8192;
   int want = (target_items + g.n_groups - 1) / g.n_groups;
@@ -1121,7 +1248,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward) {
   if (nc < 1) nc = 1;
   int tiles_per_chunk = (g.n_tiles + nc - 1) / nc;
   if (tiles_per_chunk < ch_min_tiles) tiles_per_chunk = ch_min_tiles;
-  g.CH = tiles_per_chunk * P;
+  g.CH = tiles_per_chunk * po;
   g.n_chunks = (g.Lh + g.CH - 1) / g.CH;
   g.n_items = g.n_groups * g.n_chunks;
   g.dcb = (backward && d->n_win == 1 && VISSM_BWD_DCB) ? 1 : 0;
@@ -1144,9 +1271,10 @@ struct Ws {
   float *Cp, *thp;
   float* ls_slab;                                        // fwd
   float *dC_slab, *dth_slab, *dW_slab, *halo, *wred;     // bwd
+  float* zsl;                                            // fused AR(1) ELBO: per-chunk per-sample sums
 };
 
-static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, char* base, Ws* w) {
+static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, char* base, Ws* w, bool fused = false) {
   size_t off = 0;
   auto take = [&](size_t nbytes) { char* p = base ? base + off : nullptr; off += align_up(nbytes); return p; };
   Ws t{};
@@ -1164,6 +1292,7 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
     t.dW_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_items) * n_wgrad(d) * 4));
     t.halo = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * g.n_chunks * d->k * 4));
     t.wred = reinterpret_cast<float*>(take(static_cast<size_t>(n_wgrad(d)) * 4));
+    if (fused) t.zsl = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * 4));
   }
   if (w) *w = t;
   return off;
@@ -1338,6 +1467,80 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
                      d->H, d->n_hidden, d->bn);
   VISSM_CHECK_LAUNCH("flow5_scatter");
+  return VISSM_OK;
+}
+
+
+// ---- the last AR(1) flow fused with its ELBO terms (vissm_flow_ar_elbo_fused) ----
+bool flow5_ar_fused_supports(const VissmFlowDesc* d) {
+  return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && d->n_hidden == 1 && !d->bn &&
+         !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH && d->n_win >= 1;
+}
+
+size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d) {
+  Geom g = geom(d, true, P - 1);
+  return ws_layout(d, g, true, nullptr, nullptr, true);
+}
+
+#define FLOW5_FZ_DISPATCH(JB, NP, ...)                                                     \
+  do {                                                                                     \
+    if (NP == 3) {                                                                         \
+      if (JB == 1) hipLaunchKernelGGL((bwd_kernel<1, 1, 1, 3, true>), __VA_ARGS__);        \
+      else hipLaunchKernelGGL((bwd_kernel<1, 1, 2, 3, true>), __VA_ARGS__);                \
+    } else {                                                                               \
+      if (JB == 1) hipLaunchKernelGGL((bwd_kernel<1, 1, 1, 1, true>), __VA_ARGS__);        \
+      else hipLaunchKernelGGL((bwd_kernel<1, 1, 2, 1, true>), __VA_ARGS__);                \
+    }                                                                                      \
+  } while (0)
+
+int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+                   const float* theta_term, const float* theta, const float* obs, const float* obs_bin, float obs_std,
+                   float scale, float* x, float* logsig, float* du, float* dC, float* dtheta_term,
+                   const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st) {
+  Geom g = geom(d, true, P - 1);
+  VISSM_CHECK_ARG(workspace && ws_bytes >= ws_layout(d, g, true, nullptr, nullptr, true),
+                  "flow_ar_elbo_fused: workspace too small");
+  Ws ws;
+  ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
+  launch_prep(d, w, ws, st);
+  launch_pad(d, g, C, theta_term, ws, st);
+  VISSM_CHECK_LAUNCH("flow5_fused_prep");
+  KArgs a = make_args(d, g);
+  FzArgs fz;
+  fz.theta = theta;
+  fz.obs = obs;
+  fz.bin = obs_bin;
+  fz.x = x;
+  fz.lsl = ws.zsl;
+  fz.scale = scale;
+  fz.iosd = 1.f / obs_std;
+  fz.M = d->L - d->k - 1;
+  const int32_t* wn = d->n_win > 1 ? win : nullptr;
+  prof_begin(VISSM_PROF_FLOW_BWD, st);
+  FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,
+                    static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst, du,
+                    ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
+  VISSM_CHECK_LAUNCH("flow5_fused");
+  prof_end(VISSM_PROF_FLOW_BWD, st);
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  if (rc) return rc;
+  const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
+  if (d->n_win == 1) {
+    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
+  } else {
+    rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
+  }
+  if (rc) return rc;
+  rc = launch_reduce_rows(ws.dth_slab, dtheta_term, g.n_chunks, static_cast<int64_t>(d->B) * d->H, st);
+  if (rc) return rc;
+  rc = launch_reduce_rows(ws.zsl, logsig, g.n_chunks, d->B, st);
+  if (rc) return rc;
+  const int nW = n_wgrad(d);
+  rc = launch_reduce_rows_inplace(ws.dW_slab, ws.wred, g.n_items, nW, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
+                     d->H, d->n_hidden, d->bn);
+  VISSM_CHECK_LAUNCH("flow5_fused_scatter");
   return VISSM_OK;
 }
 

@@ -24,7 +24,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import FlowShape, ma_flow, normal_base, normal_base_dev, base_logprob, elbo_terms, ElboFeeds, AdamaxKernel
+from .ops import (FlowShape, ma_flow, normal_base, normal_base_dev, base_logprob, elbo_terms, ElboFeeds,
+                  AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, tn_split_k
@@ -197,6 +198,23 @@ class IAF:
                                   p("theta1/bias"), p("theta2/kernel"), p("theta2/bias")).contiguous()
 
     # ---- per-transition part (HIP) ----
+    def weights(self):
+        """The flow kernel's weight tensors (autograd expressions of the variables): w_eps = the sample
+        channel of the first conv, stacked hidden kernels / biases / BN, head."""
+        s = self.spec
+        w_eps = self._p("conv/kernel")[:, 0, :].contiguous()
+        if s.n_hidden > 0:
+            w_hid = torch.stack([self._p(f"hidden{l}/kernel") for l in range(s.n_hidden)])
+            b_hid = torch.stack([self._p(f"hidden{l}/bias") for l in range(s.n_hidden)])
+        else:
+            w_hid = b_hid = None
+        if s.bn and s.n_hidden > 0:
+            bn_g = torch.stack([self._p(f"bn{l}/gamma") for l in range(s.n_hidden)])
+            bn_b = torch.stack([self._p(f"bn{l}/beta") for l in range(s.n_hidden)])
+        else:
+            bn_g = bn_b = None
+        return w_eps, w_hid, b_hid, bn_g, bn_b, self._p("head/kernel"), self._p("head/bias")
+
     def flow(self, shape: FlowShape, win, u, C, theta_term):
         s = self.spec
         w_eps = self._p("conv/kernel")[:, 0, :].contiguous()
@@ -276,6 +294,7 @@ class Engine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.seed = int(seed)
         self.precision = precision
+        self.fuse_last = True   # AR, bf16 / bf16x3: last flow fused with the ELBO in the training step
         H = mdef.network_dims[0]
         if any(h != H for h in mdef.network_dims):
             raise ValueError("all network_dims must be equal (the reference adds layer outputs of width network_dims[0])")
@@ -383,6 +402,72 @@ class Engine:
             elbo = scale * (sde - lq + obs) + prior - logq_theta
         return {"elbo": elbo, "sde": sde, "obs": obs, "logq": lq, "theta": theta, "logq_theta": logq_theta,
                 "prior": prior, "z": z}
+
+    # ---- the last AR(1) flow fused with its ELBO terms (training step) ----
+    def _last_shape(self, batch: Batch, B: int) -> FlowShape:
+        md = self.mdef
+        fl = self.flows[-1]
+        L = md.kernel_ext - (md.n_flows - 1) * md.k
+        return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
+                         swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+
+    def fused_ok(self, batch: Batch, B: int) -> bool:
+        """The step can run the last flow fused with the AR(1) ELBO (bf16 / bf16x3 matrix-core kernels)."""
+        if self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or not self.fuse_last:
+            return False
+        return ar_fused_supported(self._last_shape(batch, B))
+
+    def forward_fused(self, batch: Batch, eps: torch.Tensor, base_lp: Optional[torch.Tensor], x0_theta: torch.Tensor):
+        """The training step's ELBO with the last flow fused with its AR(1) ELBO terms: returns (out, (roots,
+        grads)) where out holds the per-sample ELBO and its terms (values) and
+        torch.autograd.backward(roots, grads) accumulates the gradient of -sum_b ELBO_b (AR.py:228-229): the
+        fused kernel's gradients w.r.t. its inputs (u, C, theta term, theta via sde / obs, the flow's weights)
+        enter at those tensors, the rest (earlier flows, q(theta), prior) from the scalar root."""
+        md = self.mdef
+        if base_lp is None:
+            base_lp = base_logprob(eps, md.n_logsig)
+        theta, logq_theta = self.theta_dist.sample_and_log_prob(x0_theta)
+        u, lq = eps, base_lp
+        B = eps.shape[0]
+        L = md.kernel_ext
+        for i, fl in enumerate(self.flows[:-1]):
+            F = fl.features(batch.ts[:, i * md.k:, :])
+            Lh = L - md.k
+            C = fl.conv_shared(F, Lh, 1)
+            tt = fl.theta_term(theta)
+            shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
+                              swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+            u, ls = fl.flow(shape, batch.win, u, C, tt)
+            lq = lq - ls
+            L -= md.k
+        fl = self.flows[-1]
+        i = md.n_flows - 1
+        F = fl.features(batch.ts[:, i * md.k:, :])
+        C = fl.conv_shared(F, L - md.k, 1)
+        tt = fl.theta_term(theta)
+        shape = self._last_shape(batch, B)
+        w_eps, w_hid, b_hid, _, _, w_head, b_head = fl.weights()
+        scale = md.scale_num / md.M
+        f = batch.feeds
+        x, logsig, du, dC, dtt, gw = ar_last_flow_fused(
+            shape, batch.win, u.detach().contiguous(), C.detach(), tt.detach(), theta.detach().contiguous(), f.obs,
+            f.obs_bin, md.obs_std, scale, w_eps.detach(), w_hid.detach(), b_hid.detach(), w_head.detach(),
+            b_head.detach())
+        # sde / obs from the written path and their theta gradient (x is a constant here: the fused kernel
+        # differentiated through it)
+        th = theta.detach().contiguous()
+        g = torch.full((B,), -scale, dtype=torch.float32, device=eps.device)
+        sde, obs, dth = elbo_values_and_theta_grad(md.model_id, md.M, md.dt, md.obs_std, f, x, th, g, g)
+        prior = self.prior_logprob(theta)
+        rest = scale * (-lq) + prior - logq_theta            # ELBO terms outside the fused flow (autograd)
+        # the gradient of -sum ELBO: autograd from the scalar root, the fused kernel's input gradients fed in
+        # at their tensors (a multi-root backward: no surrogate products)
+        roots = [(-rest).sum(), u, C, tt, theta, w_eps, w_hid, b_hid, w_head, b_head]
+        grads = [None, du, dC, dtt, dth] + list(gw)
+        elbo = scale * (sde + obs + logsig) + rest.detach()
+        out = {"elbo": elbo, "sde": sde, "obs": obs, "logq": (lq.detach() - logsig), "theta": th,
+               "logq_theta": logq_theta.detach(), "prior": prior.detach(), "z": x}
+        return out, (roots, grads)
 
     def prior_logprob(self, theta):
         md = self.mdef

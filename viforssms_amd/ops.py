@@ -175,6 +175,41 @@ def ma_flow(shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, 
     return MAFlowFn.apply(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
 
 
+def ar_fused_supported(shape: FlowShape) -> bool:
+    d = shape.desc()
+    return bool(_lib.load().vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)))
+
+
+def ar_last_flow_fused(shape: FlowShape, win, u, C, theta_term, theta, obs, obs_bin, obs_std: float, scale: float,
+                       w_eps, w_hid, b_hid, w_head, b_head):
+    """The last AR(1) flow fused with its ELBO terms (vissm_flow_ar_elbo_fused): one backward-style pass that
+    recomputes the flow's output x and differentiates loss = -scale sum_b (sde + obs + logsig) w.r.t. u, C,
+    theta_term and the flow's weights (no autograd: the caller routes them; the theta dependence of sde goes
+    through vissm_elbo_bwd on x).  Returns (x [B, Lout], logsig [B], du, dC, dtheta_term,
+    [g_w_eps, g_w_hid, g_b_hid, g_w_head, g_b_head])."""
+    lib = _lib.load()
+    _require_gpu(u, C, theta_term, theta, obs, obs_bin, w_eps, w_hid, b_hid, w_head, b_head, win)
+    dev = u.device
+    d = shape.desc()
+    wsz = lib.vissm_flow_ar_elbo_fused_workspace_size(ctypes.byref(d))
+    if wsz == 0:
+        raise _lib.VissmError("vissm_flow_ar_elbo_fused: unsupported flow shape")
+    ws = _workspace(wsz, dev)
+    x = torch.empty(shape.B, shape.Lout, dtype=torch.float32, device=dev)
+    logsig = torch.empty(shape.B, dtype=torch.float32, device=dev)
+    du = torch.empty_like(u)
+    dC = torch.empty_like(C)
+    dth = torch.empty_like(theta_term)
+    gw = [torch.empty_like(t) for t in (w_eps, w_hid, b_hid, w_head, b_head)]
+    grads = FlowGrads(ptr(gw[0]), ptr(gw[1]), ptr(gw[2]), None, None, ptr(gw[3]), ptr(gw[4]))
+    prm = _flow_params(w_eps, w_hid, b_hid, None, None, w_head, b_head)
+    check(lib.vissm_flow_ar_elbo_fused(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
+                                       ptr(theta), ptr(obs), ptr(obs_bin), float(obs_std), float(scale), ptr(x),
+                                       ptr(logsig), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws), wsz,
+                                       _lib.stream_handle(dev)), "vissm_flow_ar_elbo_fused")
+    return x, logsig, du, dC, dth, gw
+
+
 # ---------------------------------------------------------------------------------------
 # ELBO log-densities
 # ---------------------------------------------------------------------------------------
@@ -241,6 +276,27 @@ class ElboFn(torch.autograd.Function):
 
 def elbo_terms(model: int, M: int, dt: float, obs_std: float, feeds: ElboFeeds, z, theta):
     return ElboFn.apply(model, M, dt, obs_std, feeds, z, theta)
+
+
+def elbo_values_and_theta_grad(model: int, M: int, dt: float, obs_std: float, feeds: ElboFeeds, z, theta,
+                               g_sde: torch.Tensor, g_obs: torch.Tensor):
+    """(sde, obs) per sample and d(g_sde . sde + g_obs . obs)/d theta for a path z that is a constant (no dz:
+    vissm_elbo_bwd with dz = NULL); no autograd."""
+    lib = _lib.load()
+    _require_gpu(z, theta, g_sde, g_obs, feeds.obs, feeds.obs_bin, feeds.mask, feeds.shift, feeds.dim_one, feeds.win)
+    B = z.shape[0]
+    d = ElboDesc(model, B, M, feeds.n_win, float(dt), float(obs_std))
+    data = feeds.cdata()
+    sde = torch.empty(B, dtype=torch.float32, device=z.device)
+    obs = torch.empty_like(sde)
+    extra = torch.empty_like(sde)
+    st = _lib.stream_handle(z.device)
+    check(lib.vissm_elbo_fwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(sde), ptr(obs), ptr(extra),
+                             st), "vissm_elbo_fwd")
+    dth = torch.empty_like(theta)
+    check(lib.vissm_elbo_bwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde), ptr(g_obs),
+                             ptr(extra), None, ptr(dth), st), "vissm_elbo_bwd")
+    return sde, obs, dth
 
 
 # ---------------------------------------------------------------------------------------

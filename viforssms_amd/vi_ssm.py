@@ -133,10 +133,10 @@ class VISSMBase:
         return b
 
     # ------------------------------------------------------------------ one step
-    def forward(self, batch: Batch, step: int, eps=None, x0_theta=None, row0_dev=None):
-        """One ELBO evaluation.  eps / x0_theta inject the randomness (parity tests);
-        otherwise they are drawn from the Philox streams keyed by the global sample index
-        (row0_dev: that index's step base on the device, for a captured step)."""
+    def _draws(self, batch: Batch, step: int, eps=None, x0_theta=None, row0_dev=None):
+        """(eps, base log-prob or None, q(theta) base draw): injected (parity tests) or drawn from the Philox
+        streams keyed by the global sample index (row0_dev: that index's step base on the device, for a
+        captured step)."""
         base_lp = None
         if eps is None or x0_theta is None:
             e, blp, x0 = self.engine.draw(step, batch.B, self.dist.rank * self.p_local, self.p, row0_dev)
@@ -144,17 +144,31 @@ class VISSMBase:
                 eps, base_lp = e, blp
             if x0_theta is None:
                 x0_theta = x0
+        return eps, base_lp, x0_theta
+
+    def forward(self, batch: Batch, step: int, eps=None, x0_theta=None, row0_dev=None):
+        """One ELBO evaluation (randomness as in _draws)."""
+        eps, base_lp, x0_theta = self._draws(batch, step, eps, x0_theta, row0_dev)
         return self.engine.forward(batch, eps, base_lp, x0_theta)
 
     def elbo_step(self, batch: Batch, step: int, eps=None, x0_theta=None, apply: bool = True, row0_dev=None):
         """grad of sum(-ELBO) (AR.py:228-229) -> all-reduce -> clip_by_global_norm -> Adamax (AR.py:230-234)."""
         st = self.store
         st.zero_grad()
-        out = self.forward(batch, step, eps, x0_theta, row0_dev)
-        loss = (-out["elbo"]).sum()
-        self._arm_overlap()
-        loss.backward()
-        del loss
+        if self.engine.fused_ok(batch, batch.B):
+            # the last flow fused with the AR(1) ELBO terms (one kernel instead of the flow's forward and
+            # backward and the ELBO's dz); the multi-root backward carries the same gradient of sum(-ELBO)
+            e, bl, x0 = self._draws(batch, step, eps, x0_theta, row0_dev)
+            out, (roots, grads) = self.engine.forward_fused(batch, e, bl, x0)
+            self._arm_overlap()
+            torch.autograd.backward(roots, grads)
+            del roots, grads
+        else:
+            out = self.forward(batch, step, eps, x0_theta, row0_dev)
+            loss = (-out["elbo"]).sum()
+            self._arm_overlap()
+            loss.backward()
+            del loss
         # drop the autograd graph now: its parameter-accumulation nodes would otherwise live on into
         # the next step (and, under graph capture, run on the stream they were created on)
         out = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
