@@ -122,7 +122,8 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w,
 /* Backward of vissm_flow_fwd for a scalar loss.  du_next = dLoss/du_next (in
  * the stored, possibly swapped layout), dlogsig[b] = dLoss/dlogsig[b].
  * Writes du [B][L], dC [n_win][Lh][H], dtheta_term [B][H] and the weight
- * gradients. */
+ * gradients.  du may be NULL on the bf16 / bf16x3 kernels when the gradient
+ * w.r.t. u is not wanted (the first flow: u is the base noise). */
 int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w,
                    const float* u, const float* C, const int32_t* win,
                    const float* theta_term, const float* du_next,

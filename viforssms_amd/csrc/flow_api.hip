@@ -90,8 +90,9 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                    size_t ws_bytes, void* stream) {
   int rc = validate(d);
   if (rc) return rc;
-  VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && du && dC && dtheta_term && gr,
+  VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && dC && dtheta_term && gr,
                   "flow_bwd: null pointer");
+  VISSM_CHECK_ARG(du || use_v5(d), "flow_bwd: du may be NULL only on the bf16 / bf16x3 kernels");
   VISSM_CHECK_ARG(gr->w_eps && gr->w_head && gr->b_head && (d->n_hidden == 0 || (gr->w_hid && gr->b_hid)),
                   "flow_bwd: null grad pointer");
   VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (gr->bn_g && gr->bn_b && w->bn_g && w->bn_b),

@@ -706,7 +706,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
 // ---------------------------------------------------------------------------
 // backward kernel: one work item per wave; tiles outer, samples inner
 // ---------------------------------------------------------------------------
-template <int NH, int KB, int JB, int NP, bool FZ = false>
+template <int NH, int KB, int JB, int NP, bool FZ = false, bool DU = true>
 __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const float* __restrict__ gout, const float* __restrict__ dls,
@@ -715,6 +715,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
                                                     float* __restrict__ dth_slab, float* __restrict__ dW_slab,
                                                     float* __restrict__ halo, FzArgs fz = FzArgs{}) {
   static_assert(!FZ || NH == 1, "the fused AR(1) ELBO variant has one hidden layer");
+  // !DU (du == NULL): the gradient w.r.t. u is not wanted (the first flow's input is the base noise):
+  // the transposed convolution, its carries and the du stores are compiled out (a runtime branch
+  // around them measured 5 % slower for the launches that do need du)
+  constexpr int wdu = DU ? 1 : 0;
   constexpr int PO = FZ ? P - 1 : P;  // output positions per tile (FZ: column 15 is look-ahead only)
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
@@ -1025,7 +1029,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb) dcn[jb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < 2 * wdu; ++ks) {
         const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb)
@@ -1075,6 +1079,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           }
         }
       }
+      if constexpr (DU) {
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb)
 #pragma unroll
@@ -1082,8 +1087,9 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           const int j = 16 * jb + 4 * g + r;
           dsc[j * QW + (PADDED ? a.s * c + j : c)] = dcn[jb][r];
         }
+      }
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
-      {
+      if constexpr (DU) {
         float* db = du + static_cast<size_t>(b) * a.L;
         // fin + k <= 64 when PADDED (k <= 32), <= 96 otherwise
         constexpr int NBASE = PADDED ? 1 : 2;
@@ -1169,7 +1175,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   // ---- per-sample tails: carry -> halo / du tail; d theta -> slab ----
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
-    for (int q = lane; q < a.k; q += 64) {
+    for (int q = lane; q < a.k * wdu; q += 64) {
       const float v = mycarry[bl * KP + q];
       if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
       else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
@@ -1395,6 +1401,30 @@ size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
     }                                                                                              \
   } while (0)
 
+#define COMMA ,
+// as FLOW5_DISPATCH with trailing template arguments TAIL (write their commas as COMMA)
+#define FLOW5_DISPATCH_T(KERNEL, TAIL, NHd, JB, NP, ...)                                                  \
+  do {                                                                                             \
+    if (NP == 3) {                                                                                 \
+      if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 3, TAIL>), __VA_ARGS__);                           \
+      else hipLaunchKernelGGL((KERNEL<1, 1, 2, 3, TAIL>), __VA_ARGS__);                                   \
+    } else if (NHd == 1) {                                                                         \
+      switch (JB) {                                                                                \
+        case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 1, TAIL>), __VA_ARGS__); break;                       \
+        case 2: hipLaunchKernelGGL((KERNEL<1, 1, 2, 1, TAIL>), __VA_ARGS__); break;                       \
+        case 3: hipLaunchKernelGGL((KERNEL<1, 2, 3, 1, TAIL>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<1, 2, 4, 1, TAIL>), __VA_ARGS__); break;                      \
+      }                                                                                            \
+    } else {                                                                                       \
+      switch (JB) {                                                                                \
+        case 1: hipLaunchKernelGGL((KERNEL<3, 1, 1, 1, TAIL>), __VA_ARGS__); break;                       \
+        case 2: hipLaunchKernelGGL((KERNEL<3, 1, 2, 1, TAIL>), __VA_ARGS__); break;                       \
+        case 3: hipLaunchKernelGGL((KERNEL<3, 2, 3, 1, TAIL>), __VA_ARGS__); break;                       \
+        default: hipLaunchKernelGGL((KERNEL<3, 2, 4, 1, TAIL>), __VA_ARGS__); break;                      \
+      }                                                                                            \
+    }                                                                                              \
+  } while (0)
+
 static void launch_pad(const VissmFlowDesc* d, const Geom& g, const float* C, const float* tht, const Ws& ws,
                        hipStream_t st) {
   const int64_t nC = static_cast<int64_t>(d->n_win) * g.Lh, nT = d->B;
@@ -1445,11 +1475,17 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid(g.blocks);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
-  FLOW5_DISPATCH(bwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, du_next,
-                 dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
+  if (du)
+    FLOW5_DISPATCH_T(bwd_kernel, false COMMA true, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
+                     ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
+                     ws.halo, FzArgs{});
+  else
+    FLOW5_DISPATCH_T(bwd_kernel, false COMMA false, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
+                     ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
+                     ws.halo, FzArgs{});
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  int rc = du ? launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st) : VISSM_OK;
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {

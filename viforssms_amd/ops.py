@@ -8,6 +8,7 @@ HIP device.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -15,6 +16,9 @@ import torch
 
 from . import _lib
 from ._lib import FlowDesc, FlowParams, FlowGrads, ElboDesc, ElboData, GatherDesc, check, ptr
+
+
+_FORCE_DU = os.environ.get("VISSM_FORCE_DU") == "1"  # A/B timing hook: always compute the flows' du
 
 
 def _require_gpu(*ts):
@@ -157,7 +161,9 @@ class MAFlowFn(torch.autograd.Function):
         g_next = g_next.contiguous()
         g_ls = g_ls.contiguous()
         d = shape.desc()
-        du = torch.empty_like(u)
+        # the base noise needs no gradient: the bf16 kernels then skip the transposed convolution
+        need_du = ctx.needs_input_grad[2] or shape.precision == _lib.VISSM_PREC_FP32 or _FORCE_DU
+        du = torch.empty_like(u) if need_du else None
         dC = torch.empty_like(C)
         dth = torch.empty_like(theta_term)
         gw = [torch.empty_like(t) if t is not None else None for t in (w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)]
