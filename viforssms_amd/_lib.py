@@ -17,6 +17,9 @@ LIB_PATH = os.environ.get("VISSM_LIB", os.path.join(_HERE, "libvissm.so"))
 VISSM_PREC_FP32 = 0
 VISSM_PREC_BF16 = 1
 VISSM_PREC_BF16X3 = 2
+# host-level mode (not a C-ABI precision): forward products bf16x3 (the values that reach the ELBO: ELBO
+# within 1e-4 of the float64 oracle), backward products bf16 (gradients at bf16 accuracy)
+VISSM_PREC_BF16X3F = 3
 
 MODEL_AR, MODEL_LV, MODEL_SV, MODEL_FHN = 0, 1, 2, 3
 

@@ -384,9 +384,10 @@ class Engine:
             Lh = (L - md.k) // s
             C = fl.conv_shared(F, Lh, s)
             tt = fl.theta_term(theta)
+            pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
                               stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
-                              n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+                              n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb)
             u, ls = fl.flow(shape, batch.win, u, C, tt)
             lq = lq - ls
             L -= md.k
@@ -411,9 +412,17 @@ class Engine:
         return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
                          swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
 
+    def flow_precisions(self):
+        """(forward, backward) flow-kernel precisions of the engine's mode (VISSM_PREC_BF16X3F: bf16x3 forward
+        products, bf16 backward products)."""
+        if self.precision == _lib.VISSM_PREC_BF16X3F:
+            return _lib.VISSM_PREC_BF16X3, _lib.VISSM_PREC_BF16
+        return self.precision, None
+
     def fused_ok(self, batch: Batch, B: int) -> bool:
         """The step can run the last flow fused with the AR(1) ELBO (bf16 / bf16x3 matrix-core kernels)."""
-        if self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or not self.fuse_last:
+        if (self.mdef.family != "ar" or self.precision in (_lib.VISSM_PREC_FP32, _lib.VISSM_PREC_BF16X3F)
+                or not self.fuse_last):
             return False
         return ar_fused_supported(self._last_shape(batch, B))
 

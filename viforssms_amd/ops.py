@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
@@ -107,6 +108,7 @@ class FlowShape:
     n_logsig: int
     n_win: int
     precision: int = _lib.VISSM_PREC_FP32
+    bwd_precision: Optional[int] = None   # the backward kernel's precision when it differs (VISSM_PREC_BF16X3F)
 
     def desc(self) -> FlowDesc:
         return FlowDesc(self.B, self.L, self.k, self.H, self.n_hidden, int(self.bn), int(self.stride2),
@@ -160,6 +162,8 @@ class MAFlowFn(torch.autograd.Function):
             g_ls = torch.zeros(shape.B, dtype=torch.float32, device=dev)
         g_next = g_next.contiguous()
         g_ls = g_ls.contiguous()
+        if shape.bwd_precision is not None:
+            shape = dataclasses.replace(shape, precision=shape.bwd_precision, bwd_precision=None)
         d = shape.desc()
         # the base noise needs no gradient: the bf16 kernels then skip the transposed convolution
         need_du = ctx.needs_input_grad[2] or shape.precision == _lib.VISSM_PREC_FP32 or _FORCE_DU
