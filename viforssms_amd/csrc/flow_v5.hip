@@ -443,8 +443,22 @@ __device__ __forceinline__ void load_shared(Shared<NH, KB, JB, NP>& sh, const bf
   for (int i = threadIdx.x; i < SH::NCST; i += NT) sh.cst[i] = cst[i];
 }
 
-// transposed image: [p = 16 rows][64 h] bf16, 16 chunks of 4 per 128-byte row, chunk XOR row
-__device__ __forceinline__ int timg_off(int p, int ch) { return p * HP + 4 * (ch ^ p); }
+// transposed image: [p = 16 rows][64 h] bf16, 16 chunks of 4 per 128-byte row; chunk ch of row p
+// sits at slot ch ^ p ^ ((p & 2) << 2).  Conflict-free for all three accesses (bank rules of
+// MI355X_MICROARCH.md §LDS): the image store (ds_write_b64, 16-lane groups of one g: the XOR is a
+// bijection of p), the own-entry read (ds_read_b64, 32-lane halves: the two g of a half differ in
+// slot bit 0 and so in row parity, i.e. in the 128-B half of the bank row), and the transposed read
+// (ds_read_b64_tr_b16, 32-lane halves = rows 8h .. 8h + 7 x chunks 4hb .. 4hb + 3: the four rows of
+// one parity take four different 4-slot blocks through slot bits 2-3 = (p2, p3 ^ p1)).  The plain
+// `ch ^ p` layout (VISSM_TIMG_SWZ=0) gave the transposed reads 2-way conflicts (rows p and p ^ 2
+// shared slot blocks): SQ_LDS_BANK_CONFLICT per bf16 backward launch 2.16e8 -> 4.1e7 cycles, step
+// 118.5 -> 117.5 ms (A/B, profiles/r02/lds_swizzle_ab.log).  A full bit permutation of p that is
+// equally conflict-free cost 26 more instructions and a spill: 121.6 ms.
+#ifndef VISSM_TIMG_SWZ
+#define VISSM_TIMG_SWZ 1
+#endif
+__host__ __device__ constexpr int timg_perm(int p) { return VISSM_TIMG_SWZ ? (p ^ ((p & 2) << 2)) : p; }
+__device__ __forceinline__ int timg_off(int p, int ch) { return p * HP + 4 * (ch ^ timg_perm(p)); }
 
 template <int NP>
 __device__ __forceinline__ void put_image(__bf16* hi, __bf16* lo, const f4 (&X)[4], int g, int c) {
