@@ -206,6 +206,7 @@ constexpr int kAbl = VISSM_V5_ABLATE;
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
   int dcb;  // backward: the block's waves share a chunk and sum their dC tiles (one window)
+  int ncu;  // compute units of the device (the backward's wave priority pattern)
 };
 
 // The last flow of the AR(1) stack fused with its ELBO terms (vissm_flow_ar_elbo_fused): the backward
@@ -402,6 +403,12 @@ __device__ __forceinline__ void fence_fwd() {
 #endif
 #ifndef VISSM_BWD_FENCES
 #define VISSM_BWD_FENCES 0xff
+#endif
+#ifndef VISSM_BWD_PRIO
+#define VISSM_BWD_PRIO 1
+#endif
+#ifndef VISSM_FWD_PRIO
+#define VISSM_FWD_PRIO 0
 #endif
 #ifndef VISSM_LANE_SCALARS
 #define VISSM_LANE_SCALARS 1  // per-sample window index / d log q read once per item into lane b, then
@@ -659,6 +666,8 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][UW];
   load_shared(sh, img, cst);
+  if constexpr (VISSM_FWD_PRIO)
+    if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
@@ -755,6 +764,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   __shared__ float zls[FZ ? NW : 1][FZ ? S : 1][P];  // FZ: per-sample, per-column log sigma sums over the tiles
   __shared__ float zcar[FZ ? NW : 1][FZ ? S : 1];     // FZ: x at the previous tile's last position
   load_shared(sh, img, cst);
+  // Static wave priority.  The first dispatch round puts blocks b and b + (CU count) on one CU, so each
+  // SIMD holds one wave of a block from an even and one from an odd round; raising the priority of the
+  // odd rounds' waves lets one of the two run ahead while the other fills its stalls.  Blocks finish
+  // roughly in dispatch order, so the refills keep the pairs mixed.  Measured (AR-cfg, bf16): 29.6 ->
+  // 28.8 ms per launch; by blockIdx parity (pairs of equal priority) no change; by the wave's slot on
+  // its SIMD (hwreg HW_ID) 30.0 ms.
+  if constexpr (VISSM_BWD_PRIO)
+    if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
   if constexpr (FZ) {
     for (int i = threadIdx.x; i < NW * S * P; i += NT) (&zls[0][0][0])[i] = 0.f;
     for (int i = threadIdx.x; i < NW * S; i += NT) (&zcar[0][0])[i] = 0.f;
@@ -1318,12 +1335,25 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   return off;
 }
 
+// compute units of the current device (cached per device)
+static int device_cus() {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev < 16 && cache[dev]) return cache[dev];
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  if (dev < 16) cache[dev] = n;
+  return n;
+}
+
 static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   KArgs a;
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
   a.dcb = g.dcb;
+  a.ncu = device_cus();
   return a;
 }
 
