@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "latent-state transitions/sec (batch_dims×T per step), AR(1) T=5000, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3, "bf16x3f": 2500.0}  # MI355X dense (MI355X_MICROARCH.md);
+PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3, "bf16x3f": 2500.0, "bf16x2f": 2500.0}  # MI355X dense (MI355X_MICROARCH.md);
 # bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak
 VALU_PEAK_TFLOPS = 157.3  # fp32 vector (packed FMA) peak
 
@@ -211,7 +211,7 @@ def main():
     ap.add_argument("--M", type=int, default=None,
                     help="AR window length (reference batch_dims of AR.main; default M = T, the BASELINE workload; "
                          "hyperparameters.txt's case is --B 50 --M 50 --k 50)")
-    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3", "bf16x3f"], default="bf16",
+    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x2f"], default="bf16",
                     help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
                          "reductions and the optimizer are fp32 throughout")
     ap.add_argument("--graph", action="store_true",
@@ -240,8 +240,7 @@ def main():
     ctx = init_distributed()
     world, rank = ctx.world, ctx.rank
     dev = torch.device("cuda", torch.cuda.current_device())
-    prec = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3,
-            "bf16x3f": _lib.VISSM_PREC_BF16X3F}[args.precision]
+    prec = _lib.TRAIN_PRECISIONS[args.precision]
 
     model, meta = build_model(args, ctx, dev, prec)
     model.engine.fuse_last = args.fuse == "on"
@@ -292,12 +291,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
     elapsed, prof = timed(0)
-    # parity-precision line: the same step with bf16x3 flow products (the precision that holds the
-    # per-sample ELBO within north_star's 1e-4 of the float64 oracle), timed the same way
+    # parity-precision lines: the same step at the precisions that hold the per-sample ELBO within
+    # north_star's 1e-4 of the float64 oracle, timed the same way
     px = None
     if args.parity_line == "auto" and args.precision == "bf16" and args.model == "ar" and world == 1 and not args.graph:
         px = []
         for name, mode, note in (
+                ("bf16x2f", _lib.VISSM_PREC_BF16X2F,
+                 "forward flow products with split-bf16 weights (w_hi x + w_lo x: the weights' rounding, coherent "
+                 "over a path, removed) and bf16 activations, backward products bf16: per-sample ELBO within 1e-4 "
+                 "of the float64 oracle, gradient at bf16 accuracy (tests/test_gpu_config_parity.py)"),
                 ("bf16x3f", _lib.VISSM_PREC_BF16X3F,
                  "forward flow products bf16x3 (the values reaching the ELBO), backward products bf16: per-sample "
                  "ELBO within 1e-4 of the float64 oracle, gradient at bf16 accuracy (tests/test_gpu_config_parity.py)"),

@@ -43,6 +43,8 @@ extern "C" {
 #define VISSM_PREC_FP32 0     /* exact fp32 arithmetic */
 #define VISSM_PREC_BF16 1     /* bf16 MFMA operands, fp32 accumulation */
 #define VISSM_PREC_BF16X3 2   /* split-bf16 (hi/lo) MFMA operands: ~fp32 products */
+#define VISSM_PREC_BF16X2 3   /* forward only: split-bf16 weights, bf16 activations (two MFMAs per product);
+                                 vissm_flow_bwd / vissm_flow_ar_elbo_fused reject it */
 
 const char* vissm_last_error(void);
 int vissm_version(void);

@@ -30,14 +30,14 @@ def run(argv=None):
     hp = apply_overrides(hp, args)
 
     from viforssms_amd import ar
-    from viforssms_amd._lib import VISSM_PREC_BF16, VISSM_PREC_BF16X3, VISSM_PREC_FP32
+    from viforssms_amd._lib import TRAIN_PRECISIONS
     from viforssms_amd.data import data_gen
     from viforssms_amd.launch import barrier, init_distributed
 
     ctx = init_distributed()
     data_gen(hp.T, hp.impute, hp.x0, np.array(hp.theta), hp.obs_std, write=(ctx.rank == 0))
     barrier(ctx)
-    prec = {"fp32": VISSM_PREC_FP32, "bf16": VISSM_PREC_BF16, "bf16x3": VISSM_PREC_BF16X3}[args.precision]
+    prec = TRAIN_PRECISIONS[args.precision]
     return ar.main(hp.p, hp.kernel_len, hp.T, hp.batch_dims, hp.network_dims, hp.no_flows, hp.priors,
                    hp.feat_window, hp.x0, hp.obs_std, learn_rate=hp.learn_rate, grad_clip=hp.grad_clip,
                    max_runs=args.steps, precision=prec, dist=ctx, seed=args.seed, pre_train=not args.no_pretrain,

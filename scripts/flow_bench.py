@@ -44,7 +44,8 @@ def main():
     w_head, b_head = r(H, 2, sc=0.2), r(2, sc=0.1)
     gnext, gls = r(B, sh.Lout), r(B)
     # entries: an fp32 implementation number (1-4) or "bf16" / "bf16x3" (matrix-core bf16 kernels)
-    PREC = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3}
+    PREC = {"fp32": _lib.VISSM_PREC_FP32, "bf16": _lib.VISSM_PREC_BF16, "bf16x3": _lib.VISSM_PREC_BF16X3,
+            "bf16x2": _lib.VISSM_PREC_BF16X2}   # bf16x2: forward only (its backward runs bf16)
     impls = [x if x in PREC else "fp32" for x in (args.only or args.impls).split(",")]  # legacy 2/4 -> fp32
     import dataclasses
     res = {}
@@ -60,7 +61,8 @@ def main():
         for im in impls:
             lib.vissm_profile_reset()
             lib.vissm_profile_enable(1 if rd > 0 else 0)
-            shp = dataclasses.replace(sh, precision=PREC[im])
+            shp = dataclasses.replace(sh, precision=PREC[im],
+                                      bwd_precision=_lib.VISSM_PREC_BF16 if im == "bf16x2" else None)
             ins = [t.clone().requires_grad_(True) for t in (u, C, tt, w_eps, w_hid, b_hid, w_head, b_head)]
             extra = [bn_g, bn_b]
             torch.cuda.synchronize()

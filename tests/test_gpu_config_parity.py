@@ -18,21 +18,23 @@ execution of the oracle itself misses 1e-4).  test_ar_cfg_raw_draw keeps the raw
 kernels to a small multiple of that fp32 execution's own error instead.
 
 Tolerances as test_gpu_parity.py: fp32 / bf16x3 -- per-sample ELBO 1e-4 relative, gradient 1e-3
-relative L2, each variable 2e-2; bf16 -- 5e-3 / 5e-2 / 2e-1; bf16x3f (bf16x3 forward products, bf16
-backward products) -- ELBO 1e-4, gradient as bf16."""
+relative L2, each variable 2e-2; bf16 -- 5e-3 / 5e-2 / 2e-1; bf16x3f / bf16x2f (bf16x3 / bf16x2 forward
+products, bf16 backward products) -- ELBO 1e-4, gradient as bf16."""
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 from tests.parity_util import run_parity_case  # noqa: E402
+from viforssms_amd._lib import TRAIN_PRECISIONS as PREC  # noqa: E402
 
 DEV = "cuda:0"
-PREC = {"fp32": 0, "bf16": 1, "bf16x3": 2, "bf16x3f": 3}
 TOL = {"fp32": dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2),
        "bf16x3": dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2),
        "bf16": dict(elbo_tol=5e-3, grad_tol=5e-2, param_tol=2e-1),
        # bf16x3 forward products, bf16 backward: the ELBO at the parity bar, the gradient at bf16's
-       "bf16x3f": dict(elbo_tol=1e-4, grad_tol=5e-2, param_tol=2e-1)}
+       "bf16x3f": dict(elbo_tol=1e-4, grad_tol=5e-2, param_tol=2e-1),
+       # split-bf16 weights, bf16 activations in the forward (the weights' coherent rounding removed)
+       "bf16x2f": dict(elbo_tol=1e-4, grad_tol=5e-2, param_tol=2e-1)}
 
 
 def _check(res, elbo_tol, grad_tol, param_tol):
@@ -43,7 +45,7 @@ def _check(res, elbo_tol, grad_tol, param_tol):
     assert res["grad_max_param_err"] < param_tol, (res["worst_param"], res["grad_max_param_err"])
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16x3", "bf16", "bf16x3f"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3", "bf16", "bf16x3f", "bf16x2f"])
 def test_ar_cfg_length(prec):
     """BASELINE configs[1]: AR(1) T = 5000, impute 5, kernel_len 8 (the bench's workload), B = 20."""
     res = run_parity_case("ar", 20, 5000, 8, 3, 50, 3, 10, device=DEV, precision=PREC[prec], impute=5, condition=True)

@@ -13,6 +13,7 @@ pytestmark = pytest.mark.gpu
 
 from tests.parity_util import run_parity_case, build_model  # noqa: E402
 from oracle import nma_oracle as O  # noqa: E402
+from viforssms_amd import _lib  # noqa: E402
 
 DEV = "cuda:0"
 
@@ -69,9 +70,16 @@ def test_family_parity_multi_window(family, k, T, starts):
 # seed at 3.6e-3, scripts/bf16_err_seeds.py) and 5e-2 on the gradient.
 BF16X3_TOL = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
 BF16_TOL = dict(elbo_tol=5e-3, grad_tol=5e-2, param_tol=2e-1)
+# bf16x2f: forward products with split weights (w_hi x + w_lo x) and bf16 activations, backward bf16.  The
+# weights' rounding is the same at every position and adds up coherently over a path; the activations'
+# does not, so its share of the ELBO error shrinks with the window length and width: at the configs'
+# lengths the ELBO meets the north-star 1e-4 (test_gpu_config_parity.py; CPU emulation:
+# scripts/bf16_mix_emul.py), at these windows of tens of positions it is held to 2e-3 (between bf16's
+# 5e-3 and bf16x3's 1e-4); the gradient at bf16's
+BF16X2F_TOL = dict(elbo_tol=2e-3, grad_tol=5e-2, param_tol=2e-1)
 
 
-@pytest.mark.parametrize("prec,tol", [(2, BF16X3_TOL), (1, BF16_TOL)])
+@pytest.mark.parametrize("prec,tol", [(2, BF16X3_TOL), (1, BF16_TOL), (_lib.VISSM_PREC_BF16X2F, BF16X2F_TOL)])
 @pytest.mark.parametrize("B,M,k,nf,H,nl,fw", [
     (4, 24, 4, 2, 16, 3, 3),
     (40, 30, 8, 3, 50, 3, 10),    # AR-cfg flow shape (k = 8, H = 50, one hidden layer)

@@ -42,6 +42,24 @@ def test_library_rejects_bad_shapes_without_gpu():
     assert rc < 0 and b"bad shape" in lib.vissm_last_error()
 
 
+def test_bf16x2_is_forward_only_without_gpu():
+    """VISSM_PREC_BF16X2 (split weights, bf16 activations) runs the forward kernel; the backward entry
+    points refuse it before touching the device (include/vissm.h)."""
+    from viforssms_amd import _lib
+    lib = _lib.load()
+    d = _lib.FlowDesc(4, 40, 8, 50, 1, 0, 0, 0, 32, 1, _lib.VISSM_PREC_BF16X2, 0)
+    assert lib.vissm_flow_workspace_size(ctypes.byref(d), 0) > 0
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p).value
+    w = _lib.FlowParams(*([p] * len(_lib.FlowParams._fields_)))
+    gr = _lib.FlowGrads(*([p] * len(_lib.FlowGrads._fields_)))
+    rc = lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(w), p, p, None, p, p, p, p, p, p, ctypes.byref(gr), p, 64,
+                            None)
+    assert rc < 0 and b"forward-only" in lib.vissm_last_error()
+    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)) == 0
+    assert set(_lib.HOST_MODES) <= set(_lib.TRAIN_PRECISIONS.values())
+
+
 def _host():
     lib = ctypes.CDLL(HOSTCHECK)
     f = lib.vissm_host_trans

@@ -46,7 +46,7 @@ static int validate(const VissmFlowDesc* d) {
   VISSM_CHECK_ARG(d->n_logsig >= 0 && d->n_logsig <= d->L - d->k, "flow: bad n_logsig");
   VISSM_CHECK_ARG(d->n_win >= 1, "flow: n_win must be >= 1");
   VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32 || d->precision == VISSM_PREC_BF16 ||
-                      d->precision == VISSM_PREC_BF16X3,
+                      d->precision == VISSM_PREC_BF16X3 || d->precision == VISSM_PREC_BF16X2,
                   "flow: unknown precision %d", d->precision);
   return VISSM_OK;
 }
@@ -92,6 +92,8 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   if (rc) return rc;
   VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && dC && dtheta_term && gr,
                   "flow_bwd: null pointer");
+  VISSM_CHECK_ARG(d->precision != VISSM_PREC_BF16X2,
+                  "flow_bwd: VISSM_PREC_BF16X2 is a forward-only precision (run the backward at VISSM_PREC_BF16)");
   VISSM_CHECK_ARG(du || use_v5(d), "flow_bwd: du may be NULL only on the bf16 / bf16x3 kernels");
   VISSM_CHECK_ARG(gr->w_eps && gr->w_head && gr->b_head && (d->n_hidden == 0 || (gr->w_hid && gr->b_hid)),
                   "flow_bwd: null grad pointer");

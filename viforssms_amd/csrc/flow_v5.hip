@@ -1,9 +1,11 @@
 // IAF flow of the neural-MA sampler on the bf16 matrix cores (fp32 accumulation):
 // forward and backward.
 //
-// Precision: VISSM_PREC_BF16 (bf16 operands, one product per MFMA) or
+// Precision: VISSM_PREC_BF16 (bf16 operands, one product per MFMA),
 // VISSM_PREC_BF16X3 (split operands a = a_hi + a_lo, products a_hi b_hi + a_hi b_lo
-// + a_lo b_hi: ~2^-16 relative per product, fp32-class results).
+// + a_lo b_hi: ~2^-16 relative per product, fp32-class results), or VISSM_PREC_BF16X2 (forward
+// kernel only: split weights, bf16 activations, products w_hi x + w_lo x -- the weights' rounding
+// is the same at every position and adds up coherently over a path; the activations' is not).
 //
 // Reference: IAF._create_flow / IAF.slp (AR.py:50-89), stride-2 head
 // (lotka_volterra_partial.py:97-104), Permute fused into the store (swap_out).
@@ -55,7 +57,7 @@ typedef unsigned u2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf4 lds_bf4;
 
-// fragments: hi (and lo for NP == 3)
+// fragments: hi (and lo for NP == 3; NP == 2: lo of the weight operand only)
 template <int NP>
 struct Fr8 {
   bf8 h, l;
@@ -72,10 +74,8 @@ __device__ __forceinline__ f4 mfma16(bf4 a, bf4 b, f4 c) {
 
 template <int NP>
 __device__ __forceinline__ f4 mm(const Fr8<NP>& a, const Fr8<NP>& b, f4 c) {
-  if constexpr (NP == 3) {
-    c = mfma32(a.l, b.h, c);
-    c = mfma32(a.h, b.l, c);
-  }
+  if constexpr (NP >= 2) c = mfma32(a.l, b.h, c);  // a: the weight operand
+  if constexpr (NP == 3) c = mfma32(a.h, b.l, c);
   return mfma32(a.h, b.h, c);
 }
 template <int NP>
@@ -273,7 +273,7 @@ __device__ __forceinline__ float bias_head(const VissmFlowParams& w, int H, int 
 __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int NP, int KB, int JB,
                             bf8* __restrict__ img, float* __restrict__ cst) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
-  const int NPL = NP == 3 ? 2 : 1;
+  const int NPL = NP >= 2 ? 2 : 1;
   float v[8];
   for (int j = 0; j < 8; ++j) {
     float x = 0.f;
@@ -346,7 +346,7 @@ __global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ ds
 template <int NH, int KB, int JB, int NP>
 struct Shared {
   static constexpr int NFR = n_frags(NH, KB, JB);
-  static constexpr int NPL = NP == 3 ? 2 : 1;
+  static constexpr int NPL = NP >= 2 ? 2 : 1;
   static constexpr int NCST = (NH + 2) * HP + 4;
   bf8 img[NFR][NPL][64];
   float cst[NCST];
@@ -362,6 +362,11 @@ __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
 // launch.  (The backward keeps its fences: ~250 VGPRs leave no room to hoist anything.)
 #ifndef VISSM_FWD_REGW
 #define VISSM_FWD_REGW 1
+#endif
+// bf16x2 forward (split weights): 0 both planes in registers, 1 hi planes in registers and lo planes
+// read from LDS per use, 2 both from LDS
+#ifndef VISSM_FWD_X2
+#define VISSM_FWD_X2 1
 #endif
 #ifndef VISSM_FWD_FENCE
 #define VISSM_FWD_FENCE 0
@@ -437,7 +442,7 @@ template <int NH, int KB, int JB, int NP>
 __device__ __forceinline__ Fr8<NP> wfrag(const Shared<NH, KB, JB, NP>& sh, int f, int lane) {
   Fr8<NP> r;
   r.h = sh.img[f][0][lane];
-  if constexpr (NP == 3) r.l = sh.img[f][1][lane];
+  if constexpr (NP >= 2) r.l = sh.img[f][1][lane];
   return r;
 }
 
@@ -596,8 +601,16 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   // fragment f of the shared image, or its register copy (index i in FwdRegs order)
   auto W = [&](int f, int i) -> Fr8<NP> {
-    if constexpr (REGW) return wr->f[i];
-    else return wfrag(sh, f, lane);
+    if constexpr (REGW && NP == 2 && VISSM_FWD_X2 == 1) {  // hi planes from registers, lo planes from LDS
+      Fr8<NP> r;
+      r.h = wr->f[i].h;
+      r.l = sh.img[f][1][lane];
+      return r;
+    } else if constexpr (REGW) {
+      return wr->f[i];
+    } else {
+      return wfrag(sh, f, lane);
+    }
   };
   // layer 0: the MFMA accumulates onto C + theta (its C operand), so no separate add
   f4 acc[4];
@@ -677,7 +690,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
   float* uw = uwin[w];
 #if VISSM_FWD_REGW
-  constexpr bool REGW = true;
+  constexpr bool REGW = NP != 2 || VISSM_FWD_X2 != 2;
   FwdRegs<NH, KB, NP> wr;
 #pragma unroll
   for (int i = 0; i < 8 * NH; ++i) wr.f[i] = wfrag(sh, i, lane);
@@ -1300,7 +1313,9 @@ static int n_wgrad(const VissmFlowDesc* d) {
 }
 
 static int jb_of(int k) { return (k + 15) / 16; }
-static int np_of(const VissmFlowDesc* d) { return d->precision == VISSM_PREC_BF16X3 ? 3 : 1; }
+static int np_of(const VissmFlowDesc* d) {
+  return d->precision == VISSM_PREC_BF16X3 ? 3 : d->precision == VISSM_PREC_BF16X2 ? 2 : 1;
+}
 
 struct Ws {
   bf8* img;
@@ -1316,7 +1331,7 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   auto take = [&](size_t nbytes) { char* p = base ? base + off : nullptr; off += align_up(nbytes); return p; };
   Ws t{};
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
-  const int NPL = np_of(d) == 3 ? 2 : 1;
+  const int NPL = np_of(d) >= 2 ? 2 : 1;
   t.img = reinterpret_cast<bf8*>(take(static_cast<size_t>(n_frags(d->n_hidden, KB, JB)) * NPL * 64 * sizeof(bf8)));
   t.cst = reinterpret_cast<float*>(take(((d->n_hidden + 2) * HP + 4) * sizeof(float)));
   t.Cp = reinterpret_cast<float*>(take(static_cast<size_t>(d->n_win) * g.Lh * HP * 4));
@@ -1415,6 +1430,7 @@ bool flow5_supports(const VissmFlowDesc* d) {
   if (d->H > kMaxH || d->k > 64) return false;
   if (d->precision == VISSM_PREC_BF16) return d->n_hidden == 1 || d->n_hidden == 3;
   if (d->precision == VISSM_PREC_BF16X3) return d->n_hidden == 1 && d->k <= 32;
+  if (d->precision == VISSM_PREC_BF16X2) return d->n_hidden == 1 && d->k <= 32;  // forward kernel only
   return false;
 }
 
@@ -1498,8 +1514,17 @@ int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  FLOW5_DISPATCH(fwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst,
-                 u_next, ws.ls_slab);
+  if (np_of(d) == 2) {
+    if (jb_of(d->k) == 1)
+      hipLaunchKernelGGL((fwd_kernel<1, 1, 1, 2>), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst, u_next,
+                         ws.ls_slab);
+    else
+      hipLaunchKernelGGL((fwd_kernel<1, 1, 2, 2>), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst, u_next,
+                         ws.ls_slab);
+  } else {
+    FLOW5_DISPATCH(fwd_kernel, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img,
+                   ws.cst, u_next, ws.ls_slab);
+  }
   VISSM_CHECK_LAUNCH("flow5_fwd");
   prof_end(VISSM_PROF_FLOW_FWD, st);
   return launch_reduce_rows(ws.ls_slab, logsig, g.n_chunks, d->B, st);

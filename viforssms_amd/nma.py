@@ -413,15 +413,15 @@ class Engine:
                          swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
 
     def flow_precisions(self):
-        """(forward, backward) flow-kernel precisions of the engine's mode (VISSM_PREC_BF16X3F: bf16x3 forward
-        products, bf16 backward products)."""
-        if self.precision == _lib.VISSM_PREC_BF16X3F:
-            return _lib.VISSM_PREC_BF16X3, _lib.VISSM_PREC_BF16
+        """(forward, backward) flow-kernel precisions of the engine's mode (host modes _lib.HOST_MODES:
+        bf16x3f / bf16x2f = bf16x3 / bf16x2 forward products, bf16 backward products)."""
+        if self.precision in _lib.HOST_MODES:
+            return _lib.HOST_MODES[self.precision]
         return self.precision, None
 
     def fused_ok(self, batch: Batch, B: int) -> bool:
         """The step can run the last flow fused with the AR(1) ELBO (bf16 / bf16x3 matrix-core kernels)."""
-        if (self.mdef.family != "ar" or self.precision in (_lib.VISSM_PREC_FP32, _lib.VISSM_PREC_BF16X3F)
+        if (self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or self.precision in _lib.HOST_MODES
                 or not self.fuse_last):
             return False
         return ar_fused_supported(self._last_shape(batch, B))
