@@ -198,7 +198,7 @@ def build_model(args, ctx, dev, prec):
     return model, meta
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -224,7 +224,7 @@ def main():
     ap.add_argument("--cpu-B", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--cpu-min-steps", type=int, default=5)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     dB, dT, dk = MODEL_DEFAULTS[args.model]
     args.B = args.B or dB
     args.T = args.T or dT
@@ -232,6 +232,11 @@ def main():
     args.M = args.M or args.T
     if args.model != "ar" and args.M != args.T:
         ap.error("--M applies to the AR model only")
+    return args
+
+
+def main():
+    args = parse_args()
 
     import torch
     from viforssms_amd import _lib

@@ -254,6 +254,36 @@ int vissm_gather_windows(const VissmGatherDesc* d, const float* src, const int32
                          float* out, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * q(theta): the variational posterior over the SDE parameters (AR.py:376-391;
+ * lotka_volterra_partial.py:494-508; SV_dense.py:428-442; fitz_nag_NVP.py:480-494):
+ * n_bij bijectors Invert(MaskedAutoregressiveFlow(MADE [5, 5, 5], elu | relu)) with
+ * Permute between them over a Normal(base_loc, base_scale) base of P dimensions.
+ *   fwd: theta [B][P] = chain(x0), logq [B] = log q(theta) (base log-prob + sum of
+ *        the clipped log-scales, clip [-5, 3] straight-through).
+ *   bwd: dw += d loss / d w for d loss / d theta = dtheta and d loss / d logq = dlogq
+ *        (either may be NULL = 0); deterministic (fixed-order sums).
+ * w, mask: every bijector's MADE variables in the parameter store's order -- dense0
+ * kernel [P][5], bias [5], dense1 [5][5], bias, dense2 [5][5], bias, dense3 [5][2P],
+ * bias [2P] -- vissm_theta_num_params(P, n_bij) floats; mask holds the MADE masks in
+ * the same layout (1 on the biases).  perm[i][q]: after bijector i, z[q] <- z[perm[i][q]].
+ * ------------------------------------------------------------------------- */
+#define VISSM_THETA_MAX_P 5
+#define VISSM_THETA_MAX_BIJ 8
+typedef struct {
+  int32_t B, P, n_bij, relu;  /* relu: 0 = elu (AR / LV / FHN), 1 = relu (SV) */
+  float base_loc, base_scale;
+  int32_t perm[VISSM_THETA_MAX_BIJ - 1][VISSM_THETA_MAX_P];
+} VissmThetaDesc;
+
+int32_t vissm_theta_num_params(int32_t P, int32_t n_bij);
+size_t vissm_theta_workspace_size(const VissmThetaDesc* d);
+int vissm_theta_fwd(const VissmThetaDesc* d, const float* w, const float* mask, const float* x0,
+                    float* theta, float* logq, void* stream);
+int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, const float* x0,
+                    const float* dtheta, const float* dlogq, float* dw, void* workspace,
+                    size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing (for bench.py's live roofline): when enabled, the flow
  * entry points bracket their main kernel with hipEvents on the launch stream.
  * kind: VISSM_PROF_FLOW_FWD / VISSM_PROF_FLOW_BWD (flow kernels),

@@ -60,6 +60,14 @@ class GatherDesc(ctypes.Structure):
                 ("c_pitch", _i64), ("os_r", _i64), ("os_j", _i64), ("os_c", _i64)]
 
 
+THETA_MAX_P, THETA_MAX_BIJ = 5, 8
+
+
+class ThetaDesc(ctypes.Structure):
+    _fields_ = [("B", _i32), ("P", _i32), ("n_bij", _i32), ("relu", _i32), ("base_loc", _f32), ("base_scale", _f32),
+                ("perm", (_i32 * THETA_MAX_P) * (THETA_MAX_BIJ - 1))]
+
+
 class ElboData(ctypes.Structure):
     _fields_ = [(n, _c_void_p) for n in ("win", "obs", "obs_bin", "mask", "shift", "dim_one")]
 
@@ -95,6 +103,12 @@ SIGNATURES = {
     "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
     "vissm_gather_windows": (_i32, [ctypes.POINTER(GatherDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vissm_theta_num_params": (_i32, [_i32, _i32]),
+    "vissm_theta_workspace_size": (_size_t, [ctypes.POINTER(ThetaDesc)]),
+    "vissm_theta_fwd": (_i32, [ctypes.POINTER(ThetaDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                               _c_void_p]),
+    "vissm_theta_bwd": (_i32, [ctypes.POINTER(ThetaDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                               _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_profile_enable": (None, [_i32]),
     "vissm_profile_read": (_i32, [_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "vissm_profile_reset": (None, []),

@@ -349,3 +349,53 @@ def sqnorm(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(1, dtype=torch.float32, device=x.device)
     check(lib.vissm_sqnorm(ptr(x), n, ptr(out), ptr(ws), wsz, _lib.stream_handle(x.device)), "vissm_sqnorm")
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# q(theta) (AR.py:376-391): MAF bijectors over the base draw, one HIP launch each way
+# ---------------------------------------------------------------------------------------
+def theta_desc(B: int, P: int, n_bij: int, relu: bool, base_loc: float, base_scale: float, perms) -> "_lib.ThetaDesc":
+    if not (1 <= P <= _lib.THETA_MAX_P and 1 <= n_bij <= _lib.THETA_MAX_BIJ):
+        raise _lib.VissmError(f"q(theta): P={P}, n_bij={n_bij} outside the kernel's range")
+    d = _lib.ThetaDesc()
+    d.B, d.P, d.n_bij, d.relu = B, P, n_bij, int(bool(relu))
+    d.base_loc, d.base_scale = float(base_loc), float(base_scale)
+    for i, p in enumerate(perms):
+        for q, v in enumerate(p):
+            d.perm[i][q] = int(v)
+    return d
+
+
+class ThetaFlowFn(torch.autograd.Function):
+    """theta, log q(theta) = q(theta) sample from the base draw x0 (vissm_theta_fwd).  The backward
+    (vissm_theta_bwd) adds the MAF variables' gradient straight into `grad_slice` (the flat gradient
+    buffer's view of those variables); `anchor` is one of them, an input only so that autograd runs this
+    backward (its own gradient is part of grad_slice, so None is returned for it)."""
+
+    @staticmethod
+    def forward(ctx, desc_args, w, mask, grad_slice, x0, anchor):
+        _require_gpu(w, mask, x0)
+        lib = _lib.load()
+        B, P = x0.shape
+        d = theta_desc(B, P, *desc_args)
+        theta = torch.empty(B, P, dtype=torch.float32, device=x0.device)
+        logq = torch.empty(B, dtype=torch.float32, device=x0.device)
+        check(lib.vissm_theta_fwd(ctypes.byref(d), ptr(w), ptr(mask), ptr(x0), ptr(theta), ptr(logq),
+                                  _lib.stream_handle(x0.device)), "vissm_theta_fwd")
+        ctx.desc_args, ctx.grad_slice = desc_args, grad_slice
+        ctx.save_for_backward(w, mask, x0)
+        return theta, logq
+
+    @staticmethod
+    def backward(ctx, g_theta, g_logq):
+        w, mask, x0 = ctx.saved_tensors
+        lib = _lib.load()
+        B, P = x0.shape
+        d = theta_desc(B, P, *ctx.desc_args)
+        g_theta = g_theta.contiguous() if g_theta is not None else None
+        g_logq = g_logq.contiguous() if g_logq is not None else None
+        ws = _workspace(lib.vissm_theta_workspace_size(ctypes.byref(d)), x0.device)
+        check(lib.vissm_theta_bwd(ctypes.byref(d), ptr(w), ptr(mask), ptr(x0), ptr(g_theta), ptr(g_logq),
+                                  ptr(ctx.grad_slice), ptr(ws), ws.numel(), _lib.stream_handle(x0.device)),
+              "vissm_theta_bwd")
+        return None, None, None, None, None, None

@@ -11,7 +11,10 @@ through the bijector cache; identical in value and gradient to the explicit inve
 The MADE masks restate TF 1.8's masked_autoregressive._gen_slices/_gen_mask; log_scale is clipped
 to [-5, 3] with a straight-through gradient (_clip_by_value_preserve_grad).  These defaults are
 recalled from TF 1.8 and cannot be checked against TF offline.
-Tiny (P_theta <= 5, 580 parameters): plain torch ops on the device.
+Tiny (P_theta <= 5, 580 parameters for P = 3): the training step's sample and log q and their
+backward run as one HIP launch each (ops.ThetaFlowFn -> vissm_theta_fwd / vissm_theta_bwd, csrc/
+theta.hip) instead of ~150 small tensor kernels; `sample_and_log_prob_torch` keeps the tensor-op
+restatement, the tests' reference for the kernels.
 """
 from __future__ import annotations
 
@@ -103,8 +106,37 @@ class ThetaFlow:
         ls = ls + (torch.clamp(ls, -5.0, 3.0) - ls).detach()
         return shift, ls
 
+    def _packed(self, device):
+        """(w, grad, mask, anchor): the MAF variables as one contiguous slice of the parameter store (the
+        kernels' layout), its gradient slice, the MADE masks packed the same way, one variable of the slice."""
+        names = [f"{self.prefix}/maf{i}/dense{j}/{v}" for i in range(self.n) for j in range(len(self.masks_np))
+                 for v in ("kernel", "bias")]
+        st = self.store
+        a = st.offsets[names[0]][0]
+        b = st.offsets[names[-1]][0] + st.offsets[names[-1]][1]
+        if b - a != sum(st.offsets[n][1] for n in names) or any(
+                st.offsets[names[i + 1]][0] != st.offsets[names[i]][0] + st.offsets[names[i]][1]
+                for i in range(len(names) - 1)):
+            raise RuntimeError("q(theta) variables are not contiguous in the parameter store")
+        cache = self.__dict__.setdefault("_mask_dev", {})
+        if device not in cache:
+            parts = []
+            for _ in range(self.n):
+                for m in self.masks_np:
+                    parts += [m.reshape(-1), np.ones(m.shape[1])]
+            cache[device] = torch.tensor(np.concatenate(parts), dtype=torch.float32, device=device)
+        return st.flat[a:b], st.grad[a:b], cache[device], st.tensors[names[0]]
+
     def sample_and_log_prob(self, x0: torch.Tensor):
-        """x0: base draw [p, P] ~ N(base_loc, base_scale).  Returns theta [p, P], log q(theta) [p]."""
+        """x0: base draw [p, P] ~ N(base_loc, base_scale).  Returns theta [p, P], log q(theta) [p]
+        (vissm_theta_fwd; the backward adds the MAF variables' gradient into the store's flat gradient)."""
+        from .ops import ThetaFlowFn
+        w, g, mask, anchor = self._packed(x0.device)
+        args = (self.n, self.act is torch.relu, self.base_loc, self.base_scale, self.perms)
+        return ThetaFlowFn.apply(args, w, mask, g, x0.float().contiguous(), anchor)
+
+    def sample_and_log_prob_torch(self, x0: torch.Tensor):
+        """The same as tensor ops (the reference of the kernels in the tests)."""
         z = x0
         lq = (-0.5 * ((x0 - self.base_loc) / self.base_scale) ** 2 - math.log(self.base_scale)
               - 0.5 * math.log(2 * math.pi)).sum(-1)
