@@ -284,14 +284,11 @@ __global__ __launch_bounds__(256) void theta_bwd_kernel(VissmThetaDesc d, const 
   }
 }
 
-// dw[k] += mask[k] * sum over the slab's rows (in row order) of column k
-__global__ __launch_bounds__(256) void theta_grad_finish_kernel(const float* __restrict__ slab, int rows, int N,
+// dw[k] += mask[k] * tot[k]
+__global__ __launch_bounds__(256) void theta_grad_finish_kernel(const float* __restrict__ tot, int N,
                                                                 const float* __restrict__ m, float* __restrict__ dw) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= N) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += slab[static_cast<size_t>(r) * N + k];
-  dw[k] += s * m[k];
+  if (k < N) dw[k] += tot[k] * m[k];
 }
 
 int check_desc(const VissmThetaDesc* d) {
@@ -331,7 +328,8 @@ int32_t vissm_theta_num_params(int32_t P, int32_t n_bij) { return npb(P) * n_bij
 size_t vissm_theta_workspace_size(const VissmThetaDesc* d) {
   if (!d || d->B < 1 || d->P < 1 || d->P > VISSM_THETA_MAX_P || d->n_bij < 1) return 0;
   const size_t waves = (static_cast<size_t>(d->B) + 63) / 64;
-  return align_up(waves * npb(d->P) * d->n_bij * sizeof(float));
+  const size_t N = static_cast<size_t>(npb(d->P)) * d->n_bij;
+  return align_up(waves * N * sizeof(float)) + align_up(N * sizeof(float));  // slab, column totals
 }
 
 int vissm_theta_fwd(const VissmThetaDesc* d, const float* w, const float* mask, const float* x0, float* theta,
@@ -359,7 +357,12 @@ int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, 
   // (a partial last block: waves past B return at once; the rows of the ceil(B / 64) waves are read)
   THETA_DISPATCH(theta_bwd_kernel, d->P, grid, dim3(256), 0, st, *d, w, mask, x0, dtheta, dlogq, slab);
   VISSM_CHECK_LAUNCH("theta_bwd");
-  hipLaunchKernelGGL(theta_grad_finish_kernel, dim3((N + 255) / 256), dim3(256), 0, st, slab, waves, N, mask, dw);
+  // column totals in a fixed order (two passes: the slab is tall and narrow), then the masked add
+  float* tot = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                        align_up(static_cast<size_t>(waves) * N * sizeof(float)));
+  rc = launch_reduce_rows_inplace(slab, tot, waves, N, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(theta_grad_finish_kernel, dim3((N + 255) / 256), dim3(256), 0, st, tot, N, mask, dw);
   VISSM_CHECK_LAUNCH("theta_grad_finish");
   return VISSM_OK;
 }
