@@ -118,7 +118,11 @@ def test_model_elbo_kernels_match_oracle(model, M, n_win):
     if model != "sv":
         assert rel(obs, obs_r) < tol
     if model == "lv":
-        assert rel(ex, ex_r) < tol
+        # the Softplus ILDJ at x = softplus(z) is softplus(-z) ~ e^{-x}: where x is large (populations ~100)
+        # the float64 oracle's -log(-expm1(-x)) rounds it to 0 (as TF's fp32 does) while the kernel keeps
+        # the tiny true value, so this term is held to an absolute floor as well
+        err = float((ex.detach().double().cpu() - ex_r.detach()).abs().max())
+        assert err <= tol * float(ex_r.detach().abs().max()) + 1e-6, err
     assert torch.isfinite(zd.grad).all()
     assert rel(zd.grad, zr.grad) < 1e-4
     assert rel(thd.grad, thr.grad) < 1e-4

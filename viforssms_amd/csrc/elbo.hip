@@ -53,8 +53,10 @@ __device__ __forceinline__ void ldn(const float* __restrict__ p, float (&o)[N]) 
 }
 
 struct St {
-  float x[2];  // state
-  float j[2];  // d state / d stored z
+  float x[2];    // state
+  float j[2];    // d state / d stored z
+  float il[2];   // LV: Softplus ILDJ at the state, and its derivative w.r.t. the stored z
+  float dil[2];
 };
 
 template <int MODEL>
@@ -95,12 +97,26 @@ struct Dev<VISSM_MODEL_LV> {
     ob = a.d.obs + static_cast<size_t>(w) * 2 * M;
     bn = a.d.obs_bin + static_cast<size_t>(w) * 2 * M;
   }
-  // softplus and its derivative from one exp: e = e^{-|z|}, softplus = max(z, 0) + log1p(e)
-  __device__ static void tf(float zz, float m, float s, float* x, float* j) {
+  // softplus and its derivative from one exp: e = e^{-|z|}, softplus = max(z, 0) + log1p(e).  The ILDJ
+  // the reference adds at the transformed path, -log(1 - e^{-x}) (lotka_volterra_partial.py:294-296), is
+  // softplus(-z) = max(-z, 0) + log1p(e) where the window's mask is 1 and shift 0 (every position it
+  // covers in the reference: x = softplus(z)), with derivative sigmoid(z) - 1: no transcendental beyond
+  // the transform's own; any other mask / shift takes the general path.
+  __device__ static void tf(float zz, float m, float s, float* x, float* j, float* il, float* dil) {
     const float e = fexp(-::fabsf(zz));
-    *x = (::fmaxf(zz, 0.f) + flog1p01(e)) * m + s;
+    const float L = flog1p01(e);
+    *x = (::fmaxf(zz, 0.f) + L) * m + s;
     const float r = frcp(1.f + e);
-    *j = m * (zz >= 0.f ? r : e * r);
+    const float sg = zz >= 0.f ? r : e * r;  // sigmoid(z)
+    *j = m * sg;
+    if (m == 1.f && s == 0.f) {
+      *il = ::fmaxf(-zz, 0.f) + L;
+      *dil = sg - 1.f;
+    } else {
+      float g;
+      *il = ildj(*x, &g);
+      *dil = g * *j;
+    }
   }
   template <int N>
   __device__ void states(const float* zb, int t0, St (&o)[N]) const {
@@ -112,14 +128,14 @@ struct Dev<VISSM_MODEL_LV> {
     ldn<N>(sh + (M + 1) + t0, s1);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      tf(zz[2 * i], m0[i], s0[i], &o[i].x[0], &o[i].j[0]);
-      tf(zz[2 * i + 1], m1[i], s1[i], &o[i].x[1], &o[i].j[1]);
+      tf(zz[2 * i], m0[i], s0[i], &o[i].x[0], &o[i].j[0], &o[i].il[0], &o[i].dil[0]);
+      tf(zz[2 * i + 1], m1[i], s1[i], &o[i].x[1], &o[i].j[1], &o[i].il[1], &o[i].dil[1]);
     }
   }
   __device__ St state(const float* zb, int t) const {
     St o;
-    tf(zb[2 * t], mk[t], sh[t], &o.x[0], &o.j[0]);
-    tf(zb[2 * t + 1], mk[M + 1 + t], sh[M + 1 + t], &o.x[1], &o.j[1]);
+    tf(zb[2 * t], mk[t], sh[t], &o.x[0], &o.j[0], &o.il[0], &o.dil[0]);
+    tf(zb[2 * t + 1], mk[M + 1 + t], sh[M + 1 + t], &o.x[1], &o.j[1], &o.il[1], &o.dil[1]);
     return o;
   }
   // em::lv_trans with the exponentials hoisted, det / dt^2 = e0 x1 (Bv + e2 x2) + Bv e2 x2 (a sum of
@@ -351,10 +367,7 @@ __global__ __launch_bounds__(256) void stream_fwd_kernel(Args a, const float* __
       s_q += b0 * z0 * z0 + b1 * z1 * z1;
       s_b += b0 + b1;
     }
-    if constexpr (Dv::kExtra) {
-      float g;
-      s_e += Dv::ildj(q.x[0], &g) + Dv::ildj(q.x[1], &g);
-    }
+    if constexpr (Dv::kExtra) s_e += q.il[0] + q.il[1];
   };
   const int nfull = M / kV;  // chunks whose kV transitions all exist
   int c = lane;
@@ -441,12 +454,12 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
       g[0] += cgo * b0 * (s.x[0] - y0);
       g[1] += cgo * b1 * (s.x[1] - y1);
     }
+  };
+  // the ILDJ term observing x_e (e >= 1), already w.r.t. the stored z
+  auto ildj_dz = [&](const St& s, float& o0, float& o1) {
     if constexpr (Dv::kExtra) {
-      float d0, d1;
-      Dv::ildj(s.x[0], &d0);
-      Dv::ildj(s.x[1], &d1);
-      g[0] += ge * d0;
-      g[1] += ge * d1;
+      o0 += ge * s.dil[0];
+      o1 += ge * s.dil[1];
     }
   };
   auto head = [&](const em::TG& r, float* g) {
@@ -478,6 +491,7 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
       if constexpr (ZD == 2) {
         o[2 * j] = g[0] * st[j + 1].j[0];
         o[2 * j + 1] = g[1] * st[j + 1].j[1];
+        ildj_dz(st[j + 1], o[2 * j], o[2 * j + 1]);
       } else {
         o[j] = g[1] * st[j + 1].j[1];
       }
@@ -541,8 +555,10 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
     }
     if (!dz) continue;
     if constexpr (ZD == 2) {
-      dzb[2 * t] = g[0] * sc.j[0];
-      dzb[2 * t + 1] = g[1] * sc.j[1];
+      float o0 = g[0] * sc.j[0], o1 = g[1] * sc.j[1];
+      if (t >= 1) ildj_dz(sc, o0, o1);
+      dzb[2 * t] = o0;
+      dzb[2 * t + 1] = o1;
     } else {
       dzb[t] = g[1] * sc.j[1];
     }
