@@ -46,7 +46,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("P,n,act,B", [(3, 5, "elu", 1000), (4, 5, "relu", 65), (5, 4, "elu", 64), (3, 2, "elu", 1),
-                                       (3, 5, "elu", 65536)])
+                                       (3, 5, "elu", 65536), (2, 1, "relu", 130), (1, 3, "elu", 257)])
 def test_theta_kernels_match_tensor_ops(P, n, act, B):
     st, tf = _flow(P, n, act, seed=P + n)
     g = torch.Generator().manual_seed(7)
