@@ -110,6 +110,8 @@ constexpr float kBnScale = 0.99950037468777f;  // 1/sqrt(1 + 1e-3)
 int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipStream_t st);
 // same result, two passes for few columns / many rows; uses the slab's part-head rows as scratch
 int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hipStream_t st);
+// the same sum over a slab of bf16 partials (R rows of N bf16 at `slab`), fp32 accumulation, fixed order
+int launch_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, hipStream_t st);
 
 // flow epilogues shared by the flow implementations (flow_common.hip)
 int launch_halo_fixup(float* du, const float* halo, int B, int L, int k, int n_chunks, int s, int CH, hipStream_t st);

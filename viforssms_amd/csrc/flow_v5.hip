@@ -206,6 +206,7 @@ constexpr int kAbl = VISSM_V5_ABLATE;
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
   int dcb;  // backward: the block's waves share a chunk and sum their dC tiles (one window)
+  int dc16;  // backward, bf16 products, one window: the dC slab holds bf16 partials (half the reduce's reads)
   int ncu;  // compute units of the device (the backward's wave priority pattern)
 };
 
@@ -244,6 +245,10 @@ __device__ __forceinline__ float row_next(float v) {  // lane c <- lane c + 1 (c
 // wave skew costs the kernel 0.8 ms: measured 126.9 vs 125.8 ms per AR-cfg step, so off
 #ifndef VISSM_BWD_DCB
 #define VISSM_BWD_DCB 0
+#endif
+// bf16 dC slab partials at bf16 products, one window (read by launch_reduce_rows_bf16)
+#ifndef VISSM_BWD_DC16
+#define VISSM_BWD_DC16 1
 #endif
 
 // folded hidden weight W~_l[hin][hout] and head weight W~_h[h][o]
@@ -1196,14 +1201,26 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       }
       __syncthreads();
     } else if (c < nP) {
-      float* dcs = dC_slab + (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
+      const size_t row = (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
+      if (a.dc16) {  // (bf16 partials: each rounding is independent, the reduce sums 4096 of them in fp32)
+        __bf16* dcs = reinterpret_cast<__bf16*>(dC_slab) + row;
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int h = swz(16 * rb + 4 * g + r);
-          if (h < a.H) dcs[h] = dCa[rb][r] * kLog2e;
-        }
+          for (int r = 0; r < 4; ++r) {
+            const int h = swz(16 * rb + 4 * g + r);
+            if (h < a.H) dcs[h] = static_cast<__bf16>(dCa[rb][r] * kLog2e);
+          }
+      } else {
+        float* dcs = dC_slab + row;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = swz(16 * rb + 4 * g + r);
+            if (h < a.H) dcs[h] = dCa[rb][r] * kLog2e;
+          }
+      }
     }
   }
 
@@ -1368,6 +1385,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
   a.dcb = g.dcb;
+  a.dc16 = (VISSM_BWD_DC16 && !g.dcb && d->n_win == 1 && (d->precision == VISSM_PREC_BF16)) ? 1 : 0;
   a.ncu = device_cus();
   return a;
 }
@@ -1558,7 +1576,8 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {
-    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
+    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_dc, nC, st)
+                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
     if (rc) return rc;
   } else {
     rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
@@ -1631,7 +1650,8 @@ int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {
-    rc = launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
+    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_dc, nC, st)
+                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
   } else {
     rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
   }
