@@ -1297,6 +1297,9 @@ struct Geom {
   int blocks;     // grid size
 };
 
+#ifndef VISSM_TARGET_ITEMS
+#define VISSM_TARGET_ITEMS 8192  // work items (sample group x t-chunk) a launch aims for
+#endif
 static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   Geom g;
   g.s = d->stride2 ? 2 : 1;
@@ -1307,7 +1310,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   g.n_tiles = (g.Lh + po - 1) / po;
   int ch_min_tiles = ((d->k + g.s - 1) / g.s + po - 1) / po;
   if (ch_min_tiles < 1) ch_min_tiles = 1;
-  const int target_items = 8192;
+  const int target_items = VISSM_TARGET_ITEMS;
   int want = (target_items + g.n_groups - 1) / g.n_groups;
   int max_chunks = g.n_tiles / ch_min_tiles;
   if (max_chunks < 1) max_chunks = 1;
