@@ -415,7 +415,7 @@ __device__ __forceinline__ void fence_fwd() {
 #define VISSM_BWD_FENCES 0xff
 #endif
 #ifndef VISSM_BWD_PRIO
-#define VISSM_BWD_PRIO 1
+#define VISSM_BWD_PRIO 3
 #endif
 #ifndef VISSM_FWD_PRIO
 #define VISSM_FWD_PRIO 0
@@ -782,14 +782,25 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   __shared__ float zls[FZ ? NW : 1][FZ ? S : 1][P];  // FZ: per-sample, per-column log sigma sums over the tiles
   __shared__ float zcar[FZ ? NW : 1][FZ ? S : 1];     // FZ: x at the previous tile's last position
   load_shared(sh, img, cst);
-  // Static wave priority.  The first dispatch round puts blocks b and b + (CU count) on one CU, so each
-  // SIMD holds one wave of a block from an even and one from an odd round; raising the priority of the
-  // odd rounds' waves lets one of the two run ahead while the other fills its stalls.  Blocks finish
-  // roughly in dispatch order, so the refills keep the pairs mixed.  Measured (AR-cfg, bf16): 29.6 ->
-  // 28.8 ms per launch; by blockIdx parity (pairs of equal priority) no change; by the wave's slot on
-  // its SIMD (hwreg HW_ID) 30.0 ms.
-  if constexpr (VISSM_BWD_PRIO)
+  // Static wave priority.  Each CU holds two blocks, so each SIMD one wave of each; blocks are dispatched
+  // in rounds of (CU count) blocks and finish roughly in dispatch order, so a block of round r shares its
+  // CU with one of round r - 1 or r + 1.  VALU issue between the two waves goes by priority, then age
+  // (MI355X_MICROARCH.md, two waves per SIMD): the younger wave of a pair loses every tie and stalls.
+  // Priority = dispatch round mod 4 makes the younger wave of a pair the prioritized one (except across
+  // the wrap): 29.6 -> 28.8 ms per launch for the two-level (round & 1) form, 28.9 -> 28.8 more for mod 4;
+  // by blockIdx parity (pairs of equal priority) no change; capped at 3 (ties from round 3 on) 29.5 ms;
+  // by the wave's slot on its SIMD (hwreg HW_ID) 30.0 ms.
+  if constexpr (VISSM_BWD_PRIO == 1) {
     if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (VISSM_BWD_PRIO >= 2) {
+    // the younger block of a pair wins: priority grows with the dispatch round (blocks / CUs), capped
+    // at 3 (VISSM_BWD_PRIO 2) or wrapping mod 4 (3)
+    int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu);
+    r = VISSM_BWD_PRIO == 2 ? (r < 3 ? r : 3) : (r & 3);
+    if (r == 1) __builtin_amdgcn_s_setprio(1);
+    else if (r == 2) __builtin_amdgcn_s_setprio(2);
+    else if (r == 3) __builtin_amdgcn_s_setprio(3);
+  }
   if constexpr (FZ) {
     for (int i = threadIdx.x; i < NW * S * P; i += NT) (&zls[0][0][0])[i] = 0.f;
     for (int i = threadIdx.x; i < NW * S; i += NT) (&zcar[0][0])[i] = 0.f;
