@@ -418,7 +418,7 @@ __device__ __forceinline__ void fence_fwd() {
 #define VISSM_BWD_PRIO 3
 #endif
 #ifndef VISSM_FWD_PRIO
-#define VISSM_FWD_PRIO 0
+#define VISSM_FWD_PRIO 3  // forward: the same round-mod-4 priority (four blocks per CU): 9.45 -> 9.15 ms
 #endif
 #ifndef VISSM_LANE_SCALARS
 #define VISSM_LANE_SCALARS 1  // per-sample window index / d log q read once per item into lane b, then
@@ -684,8 +684,14 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][UW];
   load_shared(sh, img, cst);
-  if constexpr (VISSM_FWD_PRIO)
+  if constexpr (VISSM_FWD_PRIO == 1) {
     if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (VISSM_FWD_PRIO == 3) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
+    if (r == 1) __builtin_amdgcn_s_setprio(1);
+    else if (r == 2) __builtin_amdgcn_s_setprio(2);
+    else if (r == 3) __builtin_amdgcn_s_setprio(3);
+  }
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
