@@ -537,10 +537,15 @@ template <int WU>
 __device__ __forceinline__ void fetch_win(const KArgs& a, const float* __restrict__ ub, const float* __restrict__ gb,
                                           int t0, Win<WU>& wn) {
   const int lane = threadIdx.x & 63;
+  // only the entries a unit reads are fetched (u: s P + k, upstream gradient: s P); the rest of the
+  // window is zero (it meets zero weights or discarded rows).  Fetching the whole 64-entry windows
+  // re-read each row ~2.5x from beyond L2 in the backward, whose tiles-outer order revisits a
+  // sample's row 16 units later.
+  const int nu = a.s * P + a.k;
 #pragma unroll
-  for (int i = 0; i < WU; ++i) wn.u[i] = ub[clampi(t0 + 64 * i + lane, a.L)];
+  for (int i = 0; i < WU; ++i) wn.u[i] = 64 * i + lane < nu ? ub[clampi(t0 + 64 * i + lane, a.L)] : 0.f;
   wn.gv = 0.f;
-  if (gb) {
+  if (gb && lane < a.s * P) {
     const int o = t0 + lane;
     wn.gv = gb[clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
   }
