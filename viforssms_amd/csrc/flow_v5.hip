@@ -168,7 +168,14 @@ __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
 }
 __device__ __forceinline__ float softplus_fast(float x) { return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x))); }
-__device__ __forceinline__ float sigmoid_fast(float x) { return __frcp_rn(1.f + __expf(-x)); }
+#ifndef VISSM_RCP_FAST
+#define VISSM_RCP_FAST 1  // v_rcp_f32 (1 ulp) instead of the correctly rounded division sequence of __frcp_rn
+#endif
+__device__ __forceinline__ float rcp_f(float x) {
+  if constexpr (VISSM_RCP_FAST) return __builtin_amdgcn_rcpf(x);
+  else return __frcp_rn(x);
+}
+__device__ __forceinline__ float sigmoid_fast(float x) { return rcp_f(1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------
 // weight fragments (8 bf16 per lane): [frag][plane (hi, lo)][lane]
@@ -956,7 +963,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         gmu = pv ? gw[oq] : 0.f;
       }
       float dsig = gmu * uw[oq + a.k];
-      if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * __frcp_rn(sig);
+      if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig);
       const float gr = dsig * sigmoid_fast(rr);
       if (VISSM_BWD_UNCOND || g == 0) {
         gsc[w][0][c] = sig;
