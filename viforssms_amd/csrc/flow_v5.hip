@@ -167,7 +167,17 @@ __device__ __forceinline__ float elu_fast(float x) {
 __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
 }
-__device__ __forceinline__ float softplus_fast(float x) { return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x))); }
+#ifndef VISSM_SOFTPLUS_HW
+#define VISSM_SOFTPLUS_HW 1  // softplus on v_exp_f32 / v_log_f32 directly (__logf adds a denormal-scaling
+                             // and refinement sequence; 1 + e^-|x| lies in [1, 2]) and max(x, 0) as a median
+#endif
+__device__ __forceinline__ float softplus_fast(float x) {
+  if constexpr (VISSM_SOFTPLUS_HW)
+    return __builtin_amdgcn_fmed3f(x, 0.f, 3.0e38f) +
+           __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-kLog2e * fabsf(x))) * kLn2;
+  else
+    return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x)));
+}
 #ifndef VISSM_RCP_FAST
 #define VISSM_RCP_FAST 1  // v_rcp_f32 (1 ulp) instead of the correctly rounded division sequence of __frcp_rn
 #endif
@@ -411,6 +421,12 @@ __device__ __forceinline__ void fence_fwd() {
                              // elu'(I_0)), 8 dW's I_0 fragments, 16 dW_eps's u fragments, 32 the
                              // transposed conv's carry-in (measured: no further gain, off); reading
                              // the recompute's fragments a phase ahead measured no gain
+#endif
+#ifndef VISSM_BWD_DTHRMW
+#define VISSM_BWD_DTHRMW 1  // the per-sample d theta read-modify-writes branch-free, reads issued together
+#endif
+#ifndef VISSM_BWD_DUTREE
+#define VISSM_BWD_DUTREE 1  // the straight-line transposed-conv sum as reads first, then a pairwise sum
 #endif
 #ifndef VISSM_ACC_INIT
 #define VISSM_ACC_INIT 1  // layer-0 products accumulate onto C + theta
@@ -787,6 +803,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][NS][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][DTH];
+  __shared__ __attribute__((aligned(16))) float dths[NW][4];  // (VISSM_BWD_DTHRMW) sink for the rows beyond DTH
   __shared__ float carry[NW][S][KP];
   __shared__ float gsc[NW][3][P];              // sigma, d r, go even (stride 2)
   __shared__ float uwin[NW][UW];
@@ -1140,7 +1157,22 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           dWe[jb][hb] = mm<NP>(((VISSM_BWD_BATCHW & 18) == 18 && NH == 1) ? uaf[jb] : ua_frag<NP>(uw, a.s, jb, g, c), ta,
                                dWe[jb][hb]);
       }
-      if (VISSM_BWD_UNCOND || c == 0) {  // (every column of dth4 holds the same sums)
+      if (VISSM_BWD_DTHRMW && !VISSM_BWD_DTHATOM && !VISSM_BWD_UNCOND) {
+        // the four read-modify-writes with their reads issued together: rows 16 hb + 4 g beyond DTH (hb = 3,
+        // g >= 2: padding and the ones row) go to a per-wave scratch slot instead of a branch around them
+        if (c == 0) {
+          float* base = &dthl[w][bl][4 * g];
+          f4* dp[4];
+#pragma unroll
+          for (int hb = 0; hb < 4; ++hb)
+            dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
+          f4 o[4];
+#pragma unroll
+          for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
+#pragma unroll
+          for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
+        }
+      } else if (VISSM_BWD_UNCOND || c == 0) {  // (every column of dth4 holds the same sums)
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
           if (16 * hb + 4 * g < DTH) {
@@ -1181,8 +1213,22 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           if constexpr (PADDED) {
             const int qc = q < QW ? q : QW - 1;
             if (VISSM_BWD_KFIX > 0 && a.k == VISSM_BWD_KFIX) {
+              constexpr int KF = VISSM_BWD_KFIX > 0 ? VISSM_BWD_KFIX : 1;
+              if constexpr (VISSM_BWD_DUTREE) {
+                // all KF reads issued before the first add, then a pairwise sum (a chain of serial adds had
+                // the compiler wait on each read in turn)
+                float t[KF];
 #pragma unroll
-              for (int j = 0; j < (VISSM_BWD_KFIX > 0 ? VISSM_BWD_KFIX : 1); ++j) v += dsc[j * QW + qc];
+                for (int j = 0; j < KF; ++j) t[j] = dsc[j * QW + qc];
+#pragma unroll
+                for (int w2 = 1; w2 < KF; w2 *= 2)
+#pragma unroll
+                  for (int j = 0; j + w2 < KF; j += 2 * w2) t[j] += t[j + w2];
+                v = t[0];
+              } else {
+#pragma unroll
+                for (int j = 0; j < KF; ++j) v += dsc[j * QW + qc];
+              }
             } else {
 #pragma unroll 4
               for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
