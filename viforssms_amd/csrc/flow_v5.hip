@@ -430,10 +430,6 @@ __device__ __forceinline__ void fence_fwd() {
                             // dX and elu'(I_0) on the unit's dependency chain: 105.6 -> 104.3 ms per step (3;
                             // 1: 105.1, 2: 105.5; A/B, profiles/r02/dw_late_ab.log)
 #endif
-#ifndef VISSM_BWD_DTHLATE
-#define VISSM_BWD_DTHLATE 0  // (DWLATE) the d theta read-modify-writes split around the deferred dW MFMAs: 1 after
-                             // the dcon stores of the du section, 2 at their usual place
-#endif
 #ifndef VISSM_BWD_DTHRMW
 #define VISSM_BWD_DTHRMW 1  // the per-sample d theta read-modify-writes branch-free, reads issued together
 #endif
@@ -1080,7 +1076,6 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       Fr8<NP> wcp[2 * JB];  // (VISSM_BWD_BATCHW & 4: the dcon fragments, read before elu'(I_0))
       // (VISSM_BWD_DWLATE: the dZ image's four fragments; block 3 is also dW_head's B operand)
       constexpr bool DWL = VISSM_BWD_DWLATE > 0 && NH == 1 && GI && (VISSM_BWD_BATCHW & 10) == 10;
-      constexpr bool DTL = VISSM_BWD_DTHLATE > 0 && DWL && VISSM_BWD_DTHRMW && !VISSM_BWD_DTHATOM && !VISSM_BWD_UNCOND;
       Fr4<NP> dzf[4];
       auto dw_late = [&]() {
 #pragma unroll
@@ -1175,7 +1170,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       }
       // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(ih[1], il[1], D, g, c);
-      if constexpr (DWL && !DTL && VISSM_BWD_DWLATE == 1) dw_late();
+      if constexpr (DWL && VISSM_BWD_DWLATE == 1) dw_late();
       fence_bwd<5>();
       f4 dth4[4] = {};
 #pragma unroll
@@ -1187,26 +1182,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           dWe[jb][hb] = mm<NP>(((VISSM_BWD_BATCHW & 18) == 18 && NH == 1) ? uaf[jb] : ua_frag<NP>(uw, a.s, jb, g, c), ta,
                                dWe[jb][hb]);
       }
-      if constexpr (DWL && !DTL && VISSM_BWD_DWLATE == 2) dw_late();
-      // (VISSM_BWD_DTHLATE: the d theta read-modify-writes split, the reads by every lane (a broadcast per
-      //  lane group), the deferred dW MFMAs between the reads and the c = 0 writes)
-      auto dth_split = [&]() {
-        float* base = &dthl[w][bl][4 * g];
-        f4* dp[4];
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb) dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
-        f4 o[4];
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
-        dw_late();
-        if (c == 0) {
-#pragma unroll
-          for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
-        }
-      };
-      if constexpr (DTL && VISSM_BWD_DTHLATE == 2) dth_split();
-      if (DTL) {
-      } else if (VISSM_BWD_DTHRMW && !VISSM_BWD_DTHATOM && !VISSM_BWD_UNCOND) {
+      if constexpr (DWL && VISSM_BWD_DWLATE == 2) dw_late();
+      if (VISSM_BWD_DTHRMW && !VISSM_BWD_DTHATOM && !VISSM_BWD_UNCOND) {
         // the four read-modify-writes with their reads issued together: rows 16 hb + 4 g beyond DTH (hb = 3,
         // g >= 2: padding and the ones row) go to a per-wave scratch slot instead of a branch around them
         if (c == 0) {
@@ -1247,8 +1224,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           dsc[j * QW + (PADDED ? a.s * c + j : c)] = dcn[jb][r];
         }
       }
-      if constexpr (DTL && VISSM_BWD_DTHLATE == 1) dth_split();
-      if constexpr (DWL && !DTL && VISSM_BWD_DWLATE == 3) dw_late();
+      if constexpr (DWL && VISSM_BWD_DWLATE == 3) dw_late();
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       if constexpr (DU) {
         float* db = du + static_cast<size_t>(b) * a.L;
@@ -1306,7 +1282,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           else if (q < fin + a.k) mycarry[bl * KP + q - fin] = v;
         }
       }
-      if constexpr (DWL && !DTL && VISSM_BWD_DWLATE == 4) dw_late();
+      if constexpr (DWL && VISSM_BWD_DWLATE == 4) dw_late();
     }
     // tile done: its dC over the group (dcb: over the block's groups, summed through the waves'
     // image slots -- free until the next unit -- in wave order)
