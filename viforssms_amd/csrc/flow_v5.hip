@@ -430,6 +430,11 @@ __device__ __forceinline__ void fence_fwd() {
                             // dX and elu'(I_0) on the unit's dependency chain: 105.6 -> 104.3 ms per step (3;
                             // 1: 105.1, 2: 105.5; A/B, profiles/r02/dw_late_ab.log)
 #endif
+#ifndef VISSM_FZ_ZCEARLY
+#define VISSM_FZ_ZCEARLY 1  // fused AR(1) variant: the previous tile's last x (LDS carry) read with the unit's inputs:
+                            // 104.6 -> 104.2 ms per step; the log sigma column sums' read-modify-write moved to the
+                            // unit's end as well: 106.5 (A/B, profiles/r02/fz_lds_ab.log)
+#endif
 #ifndef VISSM_BWD_DTHRMW
 #define VISSM_BWD_DTHRMW 1  // the per-sample d theta read-modify-writes branch-free, reads issued together
 #endif
@@ -944,6 +949,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nZ, XN);
         stage_win<KB>(wn, uw, gw);
       }
+      // FZ (VISSM_FZ_ZCEARLY): the previous tile's last x read with the unit's inputs, not after the recompute
+      const float fz_zc = (FZ && VISSM_FZ_ZCEARLY) ? zcar[w][bl] : 0.f;
       u2 i0p[4];
       unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il, nullptr, I0R ? i0p : nullptr);
       // I_NH (the head input) with its ones row -> image NH, for dW_head
@@ -959,7 +966,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const float x = uw[c + a.k] * sig + mu;
         float xp = row_prev(x);
         const float xn = row_next(x);
-        if (c == 0) xp = zcar[w][bl];
+        if (c == 0) xp = VISSM_FZ_ZCEARLY ? fz_zc : zcar[w][bl];
         if (discard) {
           if (lane == PO - 1) zcar[w][bl] = x;
           continue;
