@@ -108,11 +108,33 @@ def _cpu_ar_step_rate(B, M, k, T, obs, ob, tt, seconds, min_steps):
     return float(np.median(steady)), len(steady), torch.get_num_threads()
 
 
+def host_cpu():
+    """The host the CPU baseline runs on: logical CPUs of the machine (os.cpu_count), CPUs this process
+    may run on (`nproc`: sched_getaffinity), the torch intra-op thread count actually used, and the
+    /proc/cpuinfo model name."""
+    import torch
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        nproc = os.cpu_count()
+    return {"cpu_model": model, "nproc": nproc, "machine_cpus": os.cpu_count(), "threads_used": torch.get_num_threads(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(args, obs, ob, tt):
     """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories."""
     B = min(args.cpu_B, args.B)
     t, n, cores = _cpu_ar_step_rate(B, args.M, args.k, args.T, obs, ob, tt, args.cpu_seconds, args.cpu_min_steps)
-    return {"value": B * args.M / t, "unit": "transitions/s", "cores": cores, "kind": "port",
+    return {"value": B * args.M / t, "unit": "transitions/s", "cores": cores, "kind": "port", "host": host_cpu(),
             "sample": f"fp32 CPU restatement of the TF1 step (oracle/nma_oracle.py) on B={B} trajectories x "
                       f"M={args.M} (T={args.T}, k={args.k}), median of {n} steps after 2 warm-up ({t:.2f} s/step)"}
 
@@ -221,6 +243,10 @@ def parse_args(argv=None):
                     help="AR at bf16 / bf16x3: run the last flow fused with the ELBO terms (vissm_flow_ar_elbo_fused)")
     ap.add_argument("--parity-line", choices=["auto", "off"], default="auto",
                     help="also time the step at bf16x3 (AR, bf16, 1 GPU) and report it as parity_precision")
+    ap.add_argument("--families", choices=["auto", "off"], default="auto",
+                    help="AR run: also time LV (every GPU count), SV and FHN (one GPU) at their per-GPU shapes "
+                         "and report them under family_lines")
+    ap.add_argument("--family-steps", type=int, default=3)
     ap.add_argument("--cpu-B", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--cpu-min-steps", type=int, default=5)
@@ -235,18 +261,17 @@ def parse_args(argv=None):
     return args
 
 
-def main():
-    args = parse_args()
-
+def measure(args, ctx, dev, parity_line: bool):
+    """Build args.model's workload, time it (warm-up, then exactly args.steps steps between barrier +
+    synchronize, max over ranks) and return the result dict (on every rank; rank 0 prints it)."""
+    import ctypes
     import torch
     from viforssms_amd import _lib
-    from viforssms_amd.launch import init_distributed
 
-    ctx = init_distributed()
     world, rank = ctx.world, ctx.rank
-    dev = torch.device("cuda", torch.cuda.current_device())
+    if world > 1:
+        import torch.distributed as dist
     prec = _lib.TRAIN_PRECISIONS[args.precision]
-
     model, meta = build_model(args, ctx, dev, prec)
     model.engine.fuse_last = args.fuse == "on"
     lib = _lib.load()
@@ -260,6 +285,9 @@ def main():
 
     if args.graph:
         args.warmup = max(args.warmup, 3)  # two eager warm-up steps, then the capture
+
+    kinds = (_lib.PROF_FLOW_FWD, _lib.PROF_FLOW_BWD, _lib.PROF_ELBO_FWD, _lib.PROF_ELBO_BWD, _lib.PROF_NORMAL,
+             _lib.PROF_FLOW_BWD_NODU, _lib.PROF_FLOW_BWD_DU, _lib.PROF_FLOW_FUSED)
 
     def timed(first_step):
         """Warm-up, then EXACTLY args.steps timed steps between barrier + synchronize on both sides;
@@ -285,21 +313,18 @@ def main():
             elapsed = float(t.item())
         tot, cnt, nbytes = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         prof = {}
-        for kind in (_lib.PROF_FLOW_FWD, _lib.PROF_FLOW_BWD, _lib.PROF_ELBO_FWD, _lib.PROF_ELBO_BWD, _lib.PROF_NORMAL):
+        for kind in kinds:
             _lib.check(lib.vissm_profile_read(kind, ctypes.byref(tot), ctypes.byref(cnt)), "profile_read")
             _lib.check(lib.vissm_profile_bytes(kind, ctypes.byref(nbytes)), "profile_bytes")
             prof[kind] = (tot.value, cnt.value, nbytes.value)
         lib.vissm_profile_reset()
         return elapsed, prof
 
-    import ctypes
-    if world > 1:
-        import torch.distributed as dist
     elapsed, prof = timed(0)
     # parity-precision lines: the same step at the precisions that hold the per-sample ELBO within
     # north_star's 1e-4 of the float64 oracle, timed the same way
     px = None
-    if args.parity_line == "auto" and args.precision == "bf16" and args.model == "ar" and world == 1 and not args.graph:
+    if parity_line and args.precision == "bf16" and args.model == "ar" and world == 1 and not args.graph:
         px = []
         for name, mode, note in (
                 ("bf16x2f", _lib.VISSM_PREC_BF16X2F,
@@ -321,15 +346,14 @@ def main():
                        "flow_fwd_avg_ms": f_ms / max(f_n, 1), "note": note})
         model.engine.precision = prec
 
-    if rank != 0:
-        return
     B, T, k, H, nh, nf, D, bn = args.B, args.M, args.k, 50, meta["nh"], meta["n_flows"], meta["D"], meta["bn"]
     kext = nf * k + D * T + D
     Lh = [(kext - i * k - k) // D for i in range(nf)]
     positions_per_launch = B * sum(Lh) / nf
     fwd_ms, fwd_n, _ = prof[_lib.PROF_FLOW_FWD]
     bwd_ms, bwd_n, _ = prof[_lib.PROF_FLOW_BWD]
-    flops_per_launch = positions_per_launch * flow_bwd_flops_per_position(k, H, nh, bn)
+    f_pos = flow_bwd_flops_per_position(k, H, nh, bn)
+    flops_per_launch = positions_per_launch * f_pos
     avg_launch_s = bwd_ms / max(bwd_n, 1) / 1e3
     achieved = flops_per_launch / avg_launch_s / 1e12 if bwd_n else None
     peak = PEAKS_TFLOPS[args.precision]
@@ -339,6 +363,24 @@ def main():
     value = world * B * T * args.steps / elapsed
     mfma_peak = PEAKS_TFLOPS[args.precision] if args.precision != "fp32" else VALU_PEAK_TFLOPS
     bwd_roof_s = mixed_roof_s(positions_per_launch, k, H, nh, bn, mfma_peak, 2)
+    # the backward launches by variant: flow 0 without du (its input is the base noise), the middle flows,
+    # and (AR, bf16 / bf16x3) the last flow fused with its ELBO terms; each with the positions of its flow
+    variants = {}
+    has_nodu, has_fused = bool(prof[_lib.PROF_FLOW_BWD_NODU][1]), bool(prof[_lib.PROF_FLOW_FUSED][1])
+    flows_of = {_lib.PROF_FLOW_BWD_NODU: [0], _lib.PROF_FLOW_FUSED: [nf - 1],
+                _lib.PROF_FLOW_BWD_DU: [i for i in range(nf) if not (i == 0 and has_nodu)
+                                        and not (i == nf - 1 and has_fused)]}
+    for kind, key in ((_lib.PROF_FLOW_BWD_NODU, "first_flow_no_du"), (_lib.PROF_FLOW_BWD_DU, "middle_flows_du"),
+                      (_lib.PROF_FLOW_FUSED, "last_flow_fused_elbo")):
+        ms, n, _ = prof[kind]
+        fl = flows_of[kind]
+        if not n or not fl:
+            continue
+        pos = B * sum(Lh[i] for i in fl) / len(fl)
+        a_ms = ms / n
+        ach = pos * f_pos / (a_ms / 1e3) / 1e12
+        variants[key] = {"avg_launch_ms": a_ms, "launches": n, "flows": fl, "achieved": ach, "frac": ach / peak,
+                         "mixed_roof_frac": mixed_roof_s(pos, k, H, nh, bn, mfma_peak, 2) / (a_ms / 1e3)}
     res = {
         "metric": METRIC if args.model == "ar" else METRIC.replace("AR(1) T=5000", f"{args.model.upper()} T={T}"),
         "value": value,
@@ -362,6 +404,7 @@ def main():
                                          "the recomputed forward is not counted",
                      "recompute_flops_per_launch": flops_per_launch / 2,
                      "avg_launch_ms": avg_launch_s * 1e3, "launches": bwd_n,
+                     "variants": variants,
                      "mixed_roof_ms": bwd_roof_s * 1e3,
                      "mixed_roof_frac": bwd_roof_s / avg_launch_s if bwd_n else None,
                      "fwd_kernel_avg_ms": fwd_ms / max(fwd_n, 1)},
@@ -369,8 +412,11 @@ def main():
     # the HBM-bound streaming kernels of the step: the algorithmic bytes each launch
     # states (libvissm records them with its HIP events: z read / dz written by the log-density kernels,
     # eps written by the base-noise kernel) over the live launch time, against the 8 TB/s HBM peak
+    fused = bool(prof[_lib.PROF_FLOW_FUSED][1])
     names = {_lib.PROF_ELBO_FWD: "elbo_fwd_kernel (log-densities: reads z)",
-             _lib.PROF_ELBO_BWD: "elbo_bwd_kernel (reads z, writes dz)",
+             _lib.PROF_ELBO_BWD: ("elbo_bwd_kernel (reads z, writes the per-sample theta gradient only: the fused "
+                                  "last flow differentiated through z itself)") if fused else
+                                 "elbo_bwd_kernel (reads z, writes dz)",
              _lib.PROF_NORMAL: "normal_base_kernel (Philox base noise: writes eps)"}
     streaming = []
     for kind, name in names.items():
@@ -398,12 +444,60 @@ def main():
                             "note": "sum of per-kernel t_min (SURVEY.md §8d) / measured step time"}
     if px is not None:
         res["parity_precision"] = px
-    if args.cpu_baseline == "auto" and world == 1 and args.model == "ar":
+    return res, model, meta
+
+
+FAMILY_NOTE = ("the other model families of BASELINE.json configs[2-4] at their per-GPU shapes, timed in the same run "
+               "the same way (warm-up, then exactly `steps` steps between barrier + synchronize, max over ranks): "
+               "LV (lotka_volterra_partial.py:402-405) at every GPU count (B = 16384 per GPU: configs[3]'s 131072 "
+               "over 8 GPUs), SV and FHN on one GPU; value = transitions/s of all ranks")
+
+
+def family_lines(args, ctx, dev):
+    """LV at every world size, SV and FHN at world 1: the families' step rates with their flow-backward
+    roofline, per-variant launch times and streaming-kernel rooflines (north_star: throughput on AR(1) /
+    Lotka-Volterra sequences at 1, 2, 4 and 8 GPUs)."""
+    import torch
+    out = []
+    models = ["lv"] + (["sv", "fhn"] if ctx.world == 1 else [])
+    for m in models:
+        a = parse_args(["--model", m, "--steps", str(args.family_steps), "--warmup", "2",
+                        "--precision", args.precision, "--cpu-baseline", "off", "--parity-line", "off"])
+        r, model, _ = measure(a, ctx, dev, parity_line=False)
+        rl = r["roofline"]
+        out.append({"model": m, "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+                    "steps": a.steps, "warmup": a.warmup, "dtype": r["dtype"], "config": r["config"],
+                    "data": r["data"],
+                    "roofline": {k: rl[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel",
+                                                    "avg_launch_ms", "fwd_kernel_avg_ms", "mixed_roof_frac",
+                                                    "variants")},
+                    "streaming_rooflines": r["streaming_rooflines"], "step_roofline": r["step_roofline"]})
+        del model
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse_args()
+
+    import torch
+    from viforssms_amd.launch import init_distributed
+
+    ctx = init_distributed()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res, model, meta = measure(args, ctx, dev, parity_line=args.parity_line == "auto")
+    if args.cpu_baseline == "auto" and ctx.world == 1 and args.model == "ar" and ctx.rank == 0:
         res["cpu_baseline"] = cpu_baseline(args, *meta["ar_data"])
         res["cpu_baseline"]["ar_plumbing"] = cpu_baseline_ar_plumbing(args)
     else:
         res["cpu_baseline"] = None
-    print(json.dumps(res), flush=True)
+    if args.families == "auto" and args.model == "ar" and not args.graph:
+        del model
+        torch.cuda.empty_cache()
+        res["family_lines"] = family_lines(args, ctx, dev)
+        res["family_lines_note"] = FAMILY_NOTE
+    if ctx.rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -94,7 +94,10 @@ typedef struct {
   int32_t n_logsig;   /* trailing outputs counted in log q: M (1-D) or 2M (2-D) */
   int32_t n_win;      /* windows in C (1 when every sample shares one window) */
   int32_t precision;  /* VISSM_PREC_* */
-  int32_t reserved;
+  int32_t chunk_tiles; /* 0 = automatic launch geometry; > 0 = head-position tiles per t-chunk of
+                          a work item (the kernel's tile size; raised to the halo minimum).  Lets a
+                          small batch run the chunk geometry of a large one: a parity test at B = 20
+                          walks the ~160-tile chunks the B = 65536 benchmark launch walks. */
 } VissmFlowDesc;
 
 typedef struct {
@@ -232,6 +235,11 @@ int vissm_sqnorm(const float* x, int64_t n, float* out, void* workspace,
 int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N,
                       void* stream);
 
+/* The same over a bf16 slab (each element widened to fp32, rows summed in order r = 0..R-1 in
+ * fp32): the flow backward's window-shared dC partials at bf16 products (one row per 16-sample
+ * group: 4096 rows at the B = 65536 benchmark), exported for its parity test. */
+int vissm_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;
  * lotka_volterra_partial.py:366-386; SV_dense.py:304-328) from device-resident
@@ -296,6 +304,12 @@ int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, 
 #define VISSM_PROF_ELBO_FWD 2
 #define VISSM_PROF_ELBO_BWD 3
 #define VISSM_PROF_NORMAL 4
+/* the flow backward launches again, by variant (each launch is also counted in VISSM_PROF_FLOW_BWD):
+ * without du (the first flow: its input is the base noise), with du (middle flows), and the last AR(1)
+ * flow fused with its ELBO terms (vissm_flow_ar_elbo_fused) */
+#define VISSM_PROF_FLOW_BWD_NODU 5
+#define VISSM_PROF_FLOW_BWD_DU 6
+#define VISSM_PROF_FLOW_FUSED 7
 void vissm_profile_enable(int32_t on);
 int vissm_profile_read(int32_t kind, double* total_ms, int64_t* count);
 void vissm_profile_reset(void);

@@ -166,6 +166,19 @@ def oracle_elbo_fp32(model, batch, eps: torch.Tensor, x0: torch.Tensor) -> np.nd
     return o["elbo"].double().numpy()
 
 
+def oracle_elbo_rows(model, starts, eps: torch.Tensor, x0: torch.Tensor) -> np.ndarray:
+    """The float64 oracle's per-sample ELBO (no gradient) for samples with window starts `starts` and
+    injected draws eps [n, kernel_ext] / x0 [n, P_theta] (float64, CPU): a sample's ELBO depends on its
+    own draws and window only, so a few rows of a large batch are checked one by one."""
+    md = model.mdef
+    spec = bridge.spec_from_mdef(md, eps.shape[0])
+    params = bridge.oracle_params(model.store.state_numpy(), spec, model.engine.theta_dist.masks_np)
+    ts, ex = oracle_inputs(model, starts)
+    with torch.no_grad():
+        o = O.elbo(spec, params, model.engine.perms, x0, eps, ts, ex)
+    return o["elbo"].double().numpy()
+
+
 def oracle_reference(model, batch, eps: torch.Tensor, x0: torch.Tensor):
     """The float64 oracle's per-sample ELBO and d sum(-ELBO) / d variable (by store name) for the
     model's current parameters, the batch's window starts and the injected eps / theta-base draws."""
@@ -188,13 +201,15 @@ def oracle_reference(model, batch, eps: torch.Tensor, x0: torch.Tensor):
 def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
                     device: str = "cuda:0", T: Optional[int] = None, starts=None, precision: int = 0,
                     seed: int = 3, impute: Optional[int] = None, condition: bool = False,
-                    fp32_yardstick: bool = False, step_path: bool = False) -> Dict:
+                    fp32_yardstick: bool = False, step_path: bool = False, chunk_tiles: int = 0) -> Dict:
     """step_path: the product side runs the training step's gradient (VI_SSM.elbo_step without the
     Adamax apply: for AR at bf16 / bf16x3 the last flow fused with the ELBO terms) instead of
-    forward + autograd backward."""
+    forward + autograd backward.  chunk_tiles > 0 forces the flow kernels' tiles per t-chunk
+    (VissmFlowDesc.chunk_tiles): the launch geometry of a larger batch at this batch."""
     torch.cuda.set_device(torch.device(device))
     model = build_model(family, B, M, k, n_flows, H, n_layers, fw, device, T=T, precision=precision, seed=seed,
                         impute=impute, condition=condition)
+    model.engine.chunk_tiles = int(chunk_tiles)
     md = model.mdef
     if starts is None:
         starts = np.zeros(B, dtype=np.int64)

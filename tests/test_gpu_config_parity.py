@@ -79,6 +79,25 @@ def test_lv_cfg_full_length():
     _check(res, **TOL["fp32"])
 
 
+# tiles per t-chunk of the B = 65536 benchmark launch (SURVEY configs[1]) on each kernel family:
+# flow5 (bf16 / bf16x3, 16-position tiles, 4096 sample groups x 2 t-chunks = 8192 work items): flows 0 / 1
+# split their 314 tiles into 2 chunks of 157 and the fused last flow its 334 into 2 of 167 -- 167 gives
+# every flow 2 chunks of 147..167 tiles at B = 20; flow4 (fp32, 32-position tiles, 2048-block target):
+# one chunk of all 157 tiles per work item.
+BENCH_CHUNK_TILES = {"fp32": 157, "bf16": 167, "bf16x3": 167, "bf16x2f": 167}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "bf16x3", "bf16x2f"])
+def test_ar_cfg_bench_geometry(prec):
+    """AR-cfg at the benchmark's launch geometry (VissmFlowDesc.chunk_tiles): at B = 20 the automatic
+    geometry cuts each work item to one tile, so this is the case where the per-sample transposed-conv
+    carries, the d theta sums and the dW accumulators run across ~160 tiles of one item on the k = 8
+    (JB = 1) kernels the headline runs."""
+    res = run_parity_case("ar", 20, 5000, 8, 3, 50, 3, 10, device=DEV, precision=PREC[prec], impute=5, condition=True,
+                          chunk_tiles=BENCH_CHUNK_TILES[prec])
+    _check(res, **TOL[prec])
+
+
 def test_ar_cfg_raw_draw():
     """AR-cfg with the unconditioned random draw (ELBO ~ -1e8..-1e10): the fp32 kernels' per-sample ELBO
     error stays within 4x (+1e-6) of what the same oracle executed in float32 (TF1's arithmetic) makes."""

@@ -23,6 +23,7 @@ CASES = [  # B, M, k, n_flows, H, n_layers, fw, T, starts
     (20, 300, 8, 3, 50, 3, 10, None, None),
     (2, 40, 32, 2, 24, 3, 4, None, None),
     (6, 30, 5, 2, 20, 3, 4, 150, [0, 30, 60, 60, 120, 0]),
+    (5, 40, 4, 1, 16, 3, 3, None, None),   # one flow: the fused flow's input is the base noise itself
 ]
 
 
@@ -48,6 +49,18 @@ def test_fused_step_ar_cfg_length(prec):
     """BASELINE configs[1] (AR(1) T = 5000, impute 5, kernel_len 8): two sample groups, many t-chunks."""
     res = run_parity_case("ar", 20, 5000, 8, 3, 50, 3, 10, device=DEV, precision=prec, impute=5, condition=True,
                           step_path=True)
+    _check(res, TOL[prec])
+
+
+@pytest.mark.parametrize("prec", [2, 1])
+def test_fused_step_ar_cfg_bench_geometry(prec):
+    """The fused kernel as the B = 65536 benchmark launches it (SURVEY configs[1]): there each 16-sample
+    group's 334 fused tiles (15 outputs each) split into 2 t-chunks of 167; VissmFlowDesc.chunk_tiles = 167
+    runs that geometry at B = 20, so the per-sample carries (transposed-conv overhang, the previous x) and
+    the dW / d theta / log sigma accumulations cross ~160 real tiles inside one work item on the k = 8 kernels
+    the benchmark uses (the automatic geometry at B = 20 cuts every chunk to one tile)."""
+    res = run_parity_case("ar", 20, 5000, 8, 3, 50, 3, 10, device=DEV, precision=prec, impute=5, condition=True,
+                          step_path=True, chunk_tiles=167)
     _check(res, TOL[prec])
 
 

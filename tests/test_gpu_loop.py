@@ -6,7 +6,8 @@ float64 oracle or an exact invariant:
   and (theta - init)^2, fitz_nag_NVP.py:288-292) and its gradient vs the oracle's, then one
   pretrain_step: Adamax(1e-3, beta1 = 0.9) from zero slots moves every variable by
   -lr * 0.1 * sign(g) per optimiser (two optimisers for SV / FHN);
-* save_paths (AR.py:323-362, lotka_volterra_partial.py:423-462): the written posterior paths for
+* save_paths (AR.py:323-362, lotka_volterra_partial.py:423-462, SV_dense.py:361-395,
+  fitz_nag_NVP.py:409-450): the written posterior paths for
   every window start vs the oracle's flow stack on the same Philox draws;
 * checkpoint: save -> perturb -> load restores params, both slot sets, the step and the numpy RNG
   (the next window draw after load equals the one after save);
@@ -119,8 +120,10 @@ def test_pretrain_loss_gradient_and_step_match_oracle(family):
     assert np.abs(delta - want)[keep].max() < 2e-6
 
 
-@pytest.mark.parametrize("family", ["ar", "lv"])
+@pytest.mark.parametrize("family", ["ar", "lv", "sv", "fhn"])
 def test_save_paths_match_oracle(family, tmp_path):
+    """save_paths (AR.py:323-362, lotka_volterra_partial.py:423-462, SV_dense.py:361-395 -- the observed
+    coordinate stacked with the transformed latent one --, fitz_nag_NVP.py:409-450) vs the oracle's paths."""
     model = _model(family)
     path = str(tmp_path / "paths.txt")
     model.save_paths(path)

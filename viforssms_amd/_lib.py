@@ -40,7 +40,7 @@ _size_t = ctypes.c_size_t
 
 class FlowDesc(ctypes.Structure):
     _fields_ = [(n, _i32) for n in ("B", "L", "k", "H", "n_hidden", "bn", "stride2", "swap_out",
-                                    "n_logsig", "n_win", "precision", "reserved")]
+                                    "n_logsig", "n_win", "precision", "chunk_tiles")]
 
 
 class FlowParams(ctypes.Structure):
@@ -102,6 +102,7 @@ SIGNATURES = {
                                          _f32, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
+    "vissm_reduce_rows_bf16": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
     "vissm_gather_windows": (_i32, [ctypes.POINTER(GatherDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_theta_num_params": (_i32, [_i32, _i32]),
     "vissm_theta_workspace_size": (_size_t, [ctypes.POINTER(ThetaDesc)]),
@@ -116,6 +117,7 @@ SIGNATURES = {
 }
 
 PROF_FLOW_FWD, PROF_FLOW_BWD, PROF_ELBO_FWD, PROF_ELBO_BWD, PROF_NORMAL = 0, 1, 2, 3, 4
+PROF_FLOW_BWD_NODU, PROF_FLOW_BWD_DU, PROF_FLOW_FUSED = 5, 6, 7
 
 
 class VissmError(RuntimeError):

@@ -48,6 +48,7 @@ static int validate(const VissmFlowDesc* d) {
   VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32 || d->precision == VISSM_PREC_BF16 ||
                       d->precision == VISSM_PREC_BF16X3 || d->precision == VISSM_PREC_BF16X2,
                   "flow: unknown precision %d", d->precision);
+  VISSM_CHECK_ARG(d->chunk_tiles >= 0, "flow: chunk_tiles=%d must be >= 0 (0 = automatic)", d->chunk_tiles);
   return VISSM_OK;
 }
 

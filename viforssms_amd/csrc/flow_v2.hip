@@ -60,6 +60,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward) {
   int nc = want < max_chunks ? want : max_chunks;
   if (nc < 1) nc = 1;
   int tiles_per_chunk = (g.n_tiles + nc - 1) / nc;
+  if (d->chunk_tiles > 0) tiles_per_chunk = d->chunk_tiles;  // caller-forced chunk geometry (tests)
   if (tiles_per_chunk < ch_min_tiles) tiles_per_chunk = ch_min_tiles;
   g.CH = tiles_per_chunk * P;
   g.n_chunks = (g.Lh + g.CH - 1) / g.CH;
@@ -764,9 +765,11 @@ int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   int hk, ks;
   buckets(d, &hk, &ks);
   prof_begin(VISSM_PROF_FLOW_BWD, st);
+  prof_begin(VISSM_PROF_FLOW_BWD_DU, st);
   FLOW2_CASES(bwd_kernel, d->n_hidden, hk, ks, grid, dim3(NT), 0, st, a, u, C, wn, theta_term, du_next, dlogsig, ws.w,
               du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo);
   VISSM_CHECK_LAUNCH("flow2_bwd");
+  prof_end(VISSM_PROF_FLOW_BWD_DU, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
   int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
   if (rc) return rc;

@@ -1427,6 +1427,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   int nc = want < max_chunks ? want : max_chunks;
   if (nc < 1) nc = 1;
   int tiles_per_chunk = (g.n_tiles + nc - 1) / nc;
+  if (d->chunk_tiles > 0) tiles_per_chunk = d->chunk_tiles;  // caller-forced chunk geometry (tests)
   if (tiles_per_chunk < ch_min_tiles) tiles_per_chunk = ch_min_tiles;
   g.CH = tiles_per_chunk * po;
   g.n_chunks = (g.Lh + g.CH - 1) / g.CH;
@@ -1674,7 +1675,9 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid(g.blocks);
+  const int pvar = du ? VISSM_PROF_FLOW_BWD_DU : VISSM_PROF_FLOW_BWD_NODU;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
+  prof_begin(pvar, st);
   if (du)
     FLOW5_DISPATCH_T(bwd_kernel, false COMMA true, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
                      ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
@@ -1684,6 +1687,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
                      ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
                      ws.halo, FzArgs{});
   VISSM_CHECK_LAUNCH("flow5_bwd");
+  prof_end(pvar, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
   int rc = du ? launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st) : VISSM_OK;
   if (rc) return rc;
@@ -1754,10 +1758,12 @@ int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   fz.M = d->L - d->k - 1;
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
+  prof_begin(VISSM_PROF_FLOW_FUSED, st);
   FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,
                     static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst, du,
                     ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
   VISSM_CHECK_LAUNCH("flow5_fused");
+  prof_end(VISSM_PROF_FLOW_FUSED, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
   int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
   if (rc) return rc;

@@ -391,6 +391,11 @@ int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, void*
   return launch_reduce_rows(slab, out, R, N, as_stream(stream));
 }
 
+int vissm_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, void* stream) {
+  VISSM_CHECK_ARG(slab && out && R >= 0 && N >= 0, "reduce_rows_bf16: bad args");
+  return launch_reduce_rows_bf16(slab, out, R, N, as_stream(stream));
+}
+
 size_t vissm_adamax_workspace_size(int64_t n) {
   (void)n;
   return align_up(kNormBlocks * sizeof(double)) + align_up(4 * sizeof(float));

@@ -59,11 +59,11 @@ class VI_SSM(VISSMBase):
 
     def pretrain_step(self, batch: Batch, run: int) -> bool:
         """t1 = minimize(lf_sample^2), t2 = minimize((theta - init)^2) each run until 500 consecutive steps
-        have a finite sde log-prob (fitz_nag_NVP.py:288-292, 372-386)."""
+        have no infinite sde log-prob (fitz_nag_NVP.py:288-292, 372-386)."""
         out = self.forward(batch, self.global_step)
         x = self.engine.lf_sample(out["z"], batch)
         target = torch.tensor(THETA_INIT, dtype=torch.float32, device=x.device)
-        finite = bool(torch.isfinite(out["sde"]).all().item())
+        finite = not bool(torch.isinf(out["sde"]).any().item())   # np.isinf only, as fitz_nag_NVP.py:378
         self.minimize_pair((x ** 2).sum(), ((out["theta"] - target) ** 2).sum())
         self.pre_train_count = self.pre_train_count + 1 if finite else 0
         return self.pre_train_count == 500

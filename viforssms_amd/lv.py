@@ -42,11 +42,12 @@ class VI_SSM(VISSMBase):
         return self.target_dims
 
     def pretrain_step(self, batch: Batch, run: int) -> bool:
-        """t1 = Adamax(1e-3, 0.9).minimize((lf_sample - 75)^2) until 1000 consecutive steps have a finite
-        lf_log_prob (lotka_volterra_partial.py:301-302, 388-400)."""
+        """t1 = Adamax(1e-3, 0.9).minimize((lf_sample - 75)^2) until 1000 consecutive steps have no infinite
+        lf_log_prob (lotka_volterra_partial.py:301-302, 388-400: the reference counts np.isinf only, so a NaN
+        does not reset the count)."""
         out = self.forward(batch, self.global_step)
         x = self.engine.lf_sample(out["z"], batch)
-        finite = bool(torch.isfinite(out["logq"]).all().item())
+        finite = not bool(torch.isinf(out["logq"]).any().item())
         self.minimize(((x - 75.0) ** 2).sum(), self._opt_pre[0], beta1=0.9, lr=1e-3)
         self.pre_train_count = self.pre_train_count + 1 if finite else 0
         return self.pre_train_count == 1000

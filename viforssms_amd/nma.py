@@ -295,6 +295,9 @@ class Engine:
         self.seed = int(seed)
         self.precision = precision
         self.fuse_last = True   # AR, bf16 / bf16x3: last flow fused with the ELBO in the training step
+        # tiles per t-chunk forced on every flow launch (VissmFlowDesc.chunk_tiles; 0 = automatic): parity tests
+        # run a large batch's launch geometry at a small batch
+        self.chunk_tiles = 0
         H = mdef.network_dims[0]
         if any(h != H for h in mdef.network_dims):
             raise ValueError("all network_dims must be equal (the reference adds layer outputs of width network_dims[0])")
@@ -387,7 +390,8 @@ class Engine:
             pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
                               stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
-                              n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb)
+                              n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
+                              chunk_tiles=self.chunk_tiles)
             u, ls = fl.flow(shape, batch.win, u, C, tt)
             lq = lq - ls
             L -= md.k
@@ -410,7 +414,8 @@ class Engine:
         fl = self.flows[-1]
         L = md.kernel_ext - (md.n_flows - 1) * md.k
         return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
-                         swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+                         swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
+                         chunk_tiles=self.chunk_tiles)
 
     def flow_precisions(self):
         """(forward, backward) flow-kernel precisions of the engine's mode (host modes _lib.HOST_MODES:
@@ -445,7 +450,8 @@ class Engine:
             C = fl.conv_shared(F, Lh, 1)
             tt = fl.theta_term(theta)
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
-                              swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision)
+                              swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
+                              chunk_tiles=self.chunk_tiles)
             u, ls = fl.flow(shape, batch.win, u, C, tt)
             lq = lq - ls
             L -= md.k
@@ -473,6 +479,9 @@ class Engine:
         # at their tensors (a multi-root backward: no surrogate products)
         roots = [(-rest).sum(), u, C, tt, theta, w_eps, w_hid, b_hid, w_head, b_head]
         grads = [None, du, dC, dtt, dth] + list(gw)
+        # only the roots that carry a gradient (a one-flow stack's u is the base noise eps: no graph behind it)
+        keep = [i for i, r in enumerate(roots) if r.requires_grad]
+        roots, grads = [roots[i] for i in keep], [grads[i] for i in keep]
         elbo = scale * (sde + obs + logsig) + rest.detach()
         out = {"elbo": elbo, "sde": sde, "obs": obs, "logq": (lq.detach() - logsig), "theta": th,
                "logq_theta": logq_theta.detach(), "prior": prior.detach(), "z": x}

@@ -109,10 +109,11 @@ class FlowShape:
     n_win: int
     precision: int = _lib.VISSM_PREC_FP32
     bwd_precision: Optional[int] = None   # the backward kernel's precision when it differs (VISSM_PREC_BF16X3F)
+    chunk_tiles: int = 0                  # VissmFlowDesc.chunk_tiles: 0 = automatic launch geometry
 
     def desc(self) -> FlowDesc:
         return FlowDesc(self.B, self.L, self.k, self.H, self.n_hidden, int(self.bn), int(self.stride2),
-                        int(self.swap_out), self.n_logsig, self.n_win, self.precision, 0)
+                        int(self.swap_out), self.n_logsig, self.n_win, self.precision, int(self.chunk_tiles))
 
     @property
     def Lout(self):
@@ -370,7 +371,12 @@ class ThetaFlowFn(torch.autograd.Function):
     """theta, log q(theta) = q(theta) sample from the base draw x0 (vissm_theta_fwd).  The backward
     (vissm_theta_bwd) adds the MAF variables' gradient straight into `grad_slice` (the flat gradient
     buffer's view of those variables); `anchor` is one of them, an input only so that autograd runs this
-    backward (its own gradient is part of grad_slice, so None is returned for it)."""
+    backward (its own gradient is part of grad_slice, so None is returned for it).
+
+    Supported use: loss.backward() into the parameter store (every VI_SSM step and pre-training minimize).
+    Under torch.autograd.grad (e.g. optimisers.AdamaxOptimizer.compute_gradients on a loss that reaches theta)
+    the q(theta) variables would come back as None while their gradient is still added into the store's flat
+    gradient; the model classes never take that route, and INTEGRATION.md states the restriction."""
 
     @staticmethod
     def forward(ctx, desc_args, w, mask, grad_slice, x0, anchor):

@@ -327,8 +327,14 @@ class VISSMBase:
         res = {}
         for i in range(theta.shape[1]):
             x = theta[:, i].exp() if pos[i] else theta[:, i]
-            stats = torch.stack([x.min(), -x.max(), x.sum(), (x * x).sum(),
-                                 torch.tensor(float(x.numel()), device=x.device)])
+            # finite entries only: a non-finite draw (a skipped step's theta, an exp overflow) must not end the
+            # loop in torch.histc; "nonfinite" counts the rest
+            ok = torch.isfinite(x)
+            xf = torch.where(ok, x, torch.zeros_like(x))
+            big = torch.finfo(x.dtype).max
+            stats = torch.stack([torch.where(ok, x, torch.full_like(x, big)).min(),
+                                 -torch.where(ok, x, torch.full_like(x, -big)).max(), xf.sum(), (xf * xf).sum(),
+                                 ok.sum().to(x.dtype), (~ok).sum().to(x.dtype)])
             if self.dist.world > 1:
                 import torch.distributed as dist
                 mm = stats[:2].clone()
@@ -336,13 +342,18 @@ class VISSMBase:
                 ss = stats[2:].clone()
                 self.dist.all_reduce_(ss)
                 stats = torch.cat([mm, ss])
-            lo, hi, s1, s2, n = stats.double().cpu().tolist()
+            lo, hi, s1, s2, n, nbad = stats.double().cpu().tolist()
             hi = -hi
-            counts = torch.histc(x, bins=bins, min=lo, max=hi if hi > lo else lo + 1.0)
+            if n > 0:
+                counts = torch.histc(x[ok], bins=bins, min=lo, max=hi if hi > lo else lo + 1.0)
+            else:
+                counts = torch.zeros(bins, device=x.device)
+                lo = hi = float("nan")
             self.dist.all_reduce_(counts)
-            mean = s1 / n
-            res[f"parameters/{i}"] = {"min": lo, "max": hi, "mean": mean, "std": max(s2 / n - mean * mean, 0.0) ** 0.5,
-                                      "count": int(n), "edges": [lo, hi], "counts": counts.cpu().tolist()}
+            mean = s1 / n if n > 0 else float("nan")
+            std = max(s2 / n - mean * mean, 0.0) ** 0.5 if n > 0 else float("nan")
+            res[f"parameters/{i}"] = {"min": lo, "max": hi, "mean": mean, "std": std, "count": int(n),
+                                      "nonfinite": int(nbad), "edges": [lo, hi], "counts": counts.cpu().tolist()}
         return res
 
     def train(self, tensorboard_path: Optional[str], save_path: Optional[str], max_runs: Optional[int] = None,
@@ -377,7 +388,10 @@ class VISSMBase:
                     out = self.elbo_step(self.batch_for(starts), self.global_step)
                 if run % self.log_every == 0:
                     self.last = self.summaries(out)
-                    hist = self.histograms(out)
+                    # histograms only for an active writer: they cost a host sync per theta component (and
+                    # collectives over ranks), which a run without a log file would pay for nothing
+                    # (decided by tensorboard_path, the same on every rank, so the ranks' collectives match)
+                    hist = self.histograms(out) if tensorboard_path else None
                     writer.write(run, self.last, hist)
             self.global_step += 1
             if run == self.early_stopping:
