@@ -51,22 +51,31 @@ def _post_stats(theta):
     return t.mean(0).cpu().numpy(), t.std(0).cpu().numpy()
 
 
-# stated tolerances (posterior mean / sd of (theta0, theta1, e^theta2), absolute, after every step):
-# fp32 kernels within 10x the float32 oracle's own drift from float64 + 2e-5; bf16x2f (bf16 backward
-# products: the gradient at bf16 accuracy) within 2e-3 absolute of the float64 trajectory
-TRAJ_TOL = {"fp32": dict(mult=10.0, floor=2e-5, elbo=1e-4), "bf16x2f": dict(mult=0.0, floor=2e-3, elbo=1e-3)}
+# stated tolerances, checked after every step:
+#  * fp32 at the paper shape (the reference's own configuration): posterior mean / sd within 10x the
+#    float32 oracle's own drift from the float64 trajectory + 2e-5 absolute, per-sample ELBO within 1e-4
+#    (or 10x the float32 oracle's error where the step's ELBO is an ill-conditioned cancellation);
+#  * bf16x2f at the AR-cfg length (BASELINE configs[1]'s window, where that precision holds the ELBO to
+#    1e-4: tests/test_gpu_config_parity.py): ELBO within 1e-4, posterior mean / sd within 2e-3 absolute
+#    (its backward products are bf16: the gradient, and so the Adamax trajectory, is bf16-accurate)
+TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance)
+    "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4),
+    "bf16x2f": (20, 5000, 8, 5000, 0.0, 2e-3, 1e-4),
+}
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16x2f"])
 def test_ar_posterior_trajectory_matches_oracle(prec):
-    K, p, M, k = 20, 50, 50, 50
-    tol = TRAJ_TOL[prec]
-    model = build_model("ar", p, M, k, 3, 50, 3, 10, DEV, T=5000, precision=PREC[prec], impute=1, condition=True)
+    K = 20
+    p, M, k, T, mult, floor, elbo_tol = TRAJ[prec]
+    model = build_model("ar", p, M, k, 3, 50, 3, 10, DEV, T=T, precision=PREC[prec], impute=1 if M < T else 5,
+                        condition=True)
     md = model.mdef
     model.grad_clip, model.learn_rate = 2.5e8, 1e-3
     spec = bridge.spec_from_mdef(md, p)
     P = {64: bridge.oracle_params(model.store.state_numpy(), spec, model.engine.theta_dist.masks_np)}
-    P[32] = _cast(P[64], torch.float32)
+    if mult > 0:
+        P[32] = _cast(P[64], torch.float32)
     S = {d: [(torch.zeros_like(t), torch.zeros_like(t)) for t in O.param_leaves(P[d])] for d in P}
     g = torch.Generator().manual_seed(17)
     xe = torch.randn(N_POST, md.P_theta, generator=g, dtype=torch.float64) * md.theta_base[1] + md.theta_base[0]
@@ -94,33 +103,41 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
         torch.cuda.synchronize()
         ts, ex = oracle_inputs(model, starts)
         info = {}
-        for d, dt in ((64, torch.float64), (32, torch.float32)):
+        for d in P:
+            dt = torch.float64 if d == 64 else torch.float32
             new, S[d], info[d] = O.train_step(spec, P[d], S[d], model.engine.perms, x0.to(dt), eps.to(dt),
                                               ts.to(dt), {kk: v.to(dt) for kk, v in ex.items()}, 1e-3, clip=2.5e8)
             P[d] = _rebuild(P[d], new)
         e64 = info[64]["elbo"].double().numpy()
-        e32 = info[32]["elbo"].double().numpy()
         eg = out["elbo"].double().cpu().numpy()
-        (ma, sa), (mb, sb), (mg, sg) = post_oracle(P[64], torch.float64), post_oracle(P[32], torch.float32), post_gpu()
-        d32m, d32s = np.abs(mb - ma).max(), np.abs(sb - sa).max()
+        ma, sa = post_oracle(P[64], torch.float64)
+        mg, sg = post_gpu()
         dgm, dgs = np.abs(mg - ma).max(), np.abs(sg - sa).max()
         erel = float(np.max(np.abs(eg - e64) / np.abs(e64)))
-        erel32 = float(np.max(np.abs(e32 - e64) / np.abs(e64)))
+        if 32 in P:
+            mb, sb = post_oracle(P[32], torch.float32)
+            d32m, d32s = np.abs(mb - ma).max(), np.abs(sb - sa).max()
+            erel32 = float(np.max(np.abs(info[32]["elbo"].double().numpy() - e64) / np.abs(e64)))
+        else:
+            d32m = d32s = erel32 = 0.0
         print(f"step {step}: mean64 {np.round(ma, 5)} move {np.abs(ma - m0).max():.2e} | gpu dmean {dgm:.2e} dsd "
               f"{dgs:.2e} elbo {erel:.2e} | fp32-oracle dmean {d32m:.2e} dsd {d32s:.2e} elbo {erel32:.2e}", flush=True)
         assert np.isfinite(eg).all() and np.isfinite(mg).all()
-        assert dgm <= tol["mult"] * d32m + tol["floor"], (step, dgm, d32m)
-        assert dgs <= tol["mult"] * d32s + tol["floor"], (step, dgs, d32s)
-        assert erel <= max(tol["elbo"], 10 * erel32), (step, erel, erel32)
+        assert dgm <= mult * d32m + floor, (step, dgm, d32m)
+        assert dgs <= mult * d32s + floor, (step, dgs, d32s)
+        assert erel <= max(elbo_tol, 10 * erel32), (step, erel, erel32)
         worst = {"dmean": max(worst["dmean"], dgm), "dsd": max(worst["dsd"], dgs), "elbo": max(worst["elbo"], erel)}
     print("worst over the trajectory:", worst)
-    # the trajectory moved the posterior far more than the tolerance (the comparison is not vacuous)
-    assert np.abs(ma - m0).max() > 20 * tol["floor"]
+    # the trajectory moved the posterior by more than the tolerance (the comparison is not vacuous)
+    assert np.abs(ma - m0).max() > 5 * floor
 
 
-RECOVERY_STEPS = int(os.environ.get("VISSM_RECOVERY_STEPS", "20000"))
-# stated band for the posterior mean after RECOVERY_STEPS (generating values 5, 0.5, 3)
-RECOVERY_BAND = {"theta0": (5.0, 1.0), "theta1": (0.5, 0.1), "e^theta2": (3.0, 0.5)}
+RECOVERY_STEPS = int(os.environ.get("VISSM_RECOVERY_STEPS", "10000"))
+# stated band for the posterior mean after RECOVERY_STEPS ELBO steps (generating values 5, 0.5, 3; measured:
+# (5.00, 0.504, 3.02) with sd (0.20, 0.016, 0.035) after 7000 steps, (5.05, 0.502, 3.02) after 30000,
+# gpurun_out record in profiles/r03/ar_recovery.log), and the posterior sd below which it must have concentrated
+RECOVERY_BAND = {"theta0": (5.0, 0.5), "theta1": (0.5, 0.05), "e^theta2": (3.0, 0.15)}
+RECOVERY_SD_MAX = (0.5, 0.05, 0.15)
 
 
 def test_ar_posterior_recovers_generating_theta():
@@ -137,3 +154,5 @@ def test_ar_posterior_recovers_generating_theta():
                                     for r in recs])
     for (name, (truth, band)), v in zip(RECOVERY_BAND.items(), m):
         assert abs(v - truth) <= band, (name, v, truth, band)
+    for v, smax in zip(recs[-1]["sd"], RECOVERY_SD_MAX):
+        assert v < smax, (recs[-1]["sd"], RECOVERY_SD_MAX)

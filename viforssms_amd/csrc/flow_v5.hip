@@ -487,13 +487,13 @@ __device__ __forceinline__ Fr8<NP> wfrag(const Shared<NH, KB, JB, NP>& sh, int f
   return r;
 }
 
-template <int NH, int KB, int JB, int NP>
+template <int NH, int KB, int JB, int NP, int NTHR = NT>
 __device__ __forceinline__ void load_shared(Shared<NH, KB, JB, NP>& sh, const bf8* __restrict__ img,
                                             const float* __restrict__ cst) {
   using SH = Shared<NH, KB, JB, NP>;
   constexpr int N = SH::NFR * SH::NPL * 64;
-  for (int i = threadIdx.x; i < N; i += NT) (&sh.img[0][0][0])[i] = img[i];
-  for (int i = threadIdx.x; i < SH::NCST; i += NT) sh.cst[i] = cst[i];
+  for (int i = threadIdx.x; i < N; i += NTHR) (&sh.img[0][0][0])[i] = img[i];
+  for (int i = threadIdx.x; i < SH::NCST; i += NTHR) sh.cst[i] = cst[i];
 }
 
 // transposed image: [p = 16 rows][64 h] bf16, 16 chunks of 4 per 128-byte row; chunk ch of row p
@@ -1399,6 +1399,525 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 }
 
 // ---------------------------------------------------------------------------
+// backward kernel, two samples per unit ("bwd2"): the AR configurations' flow shape (one hidden layer,
+// bf16 products, k <= KP2, stride 1, one window)
+//
+// A unit is (two samples of the group) x (tile of 16 head positions).  The two samples' dependency chains
+// (recompute -> head backward -> dX -> dA0 -> dcon -> transposed conv) run interleaved in one wave, so each
+// covers the other's MFMA and LDS latencies; the weight fragments, the C rows and the dC tile accumulator
+// are shared by the pair; and every product that contracts over positions (dW, dW_head, dW_eps, d theta)
+// contracts over the pair's 32 columns with one v_mfma_f32_16x16x32_bf16 (K = 32: k = 8g + jj is sample
+// jj >> 2, position 4g + (jj & 3), i.e. the two samples' ds_read_b64_tr_b16 fragments side by side), half
+// the 16x16x16 instructions of the one-sample kernel at the same matrix-pipe cycles each.  d theta is per
+// sample: one MFMA against a ones operand split by sample (columns 0-7 sample A, 8-15 sample B).
+// Blocks of 8 waves (one block per CU, two waves per SIMD) stage the weight images once.
+// A group with an odd sample count pairs its last sample with a ghost (sample A again, upstream gradient
+// zero: every contribution of the ghost is exactly zero and its stores are skipped).
+// ---------------------------------------------------------------------------
+constexpr int NW2 = 8;
+constexpr int NT2 = 64 * NW2;
+constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
+#ifndef VISSM_BWD2
+#define VISSM_BWD2 1
+#endif
+#ifndef VISSM_BWD2_PRIO
+#define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
+#endif
+
+// the K = 32 fragment of a position contraction: sample A's transposed fragment then sample B's
+__device__ __forceinline__ bf8 cat8(bf4 a, bf4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf8 tr_frag2(const __bf16* img, int hb, int g, int c) {
+  return cat8(tr_read(img, hb, g, c), tr_read(img + P * HP, hb, g, c));
+}
+
+template <bool FZ, bool DU>
+__global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+                                                      const float* __restrict__ tht, const float* __restrict__ gout,
+                                                      const float* __restrict__ dls, const bf8* __restrict__ img,
+                                                      const float* __restrict__ cst, float* __restrict__ du,
+                                                      float* __restrict__ dC_slab, float* __restrict__ dth_slab,
+                                                      float* __restrict__ dW_slab, float* __restrict__ halo,
+                                                      FzArgs fz = FzArgs{}) {
+  constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
+  constexpr int PO = FZ ? P - 1 : P;
+  constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
+  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ __bf16 timg[NW2][2][2 * P * HP];  // [wave][slot][row 16 cb + position][64 h]
+  __shared__ float dthl[NW2][S][DTH];
+  __shared__ __attribute__((aligned(16))) float dths[NW2][4];
+  __shared__ float carry[NW2][S][KP2];
+  __shared__ float gsc[NW2][2][P];
+  __shared__ float uwin[NW2][2][64];
+  __shared__ float gwin[NW2][2][P];
+  __shared__ float dscr[NW2][2][KP2][QW2];
+  __shared__ float zls[FZ ? NW2 : 1][FZ ? S : 1][P];
+  __shared__ float zcar[FZ ? NW2 : 1][FZ ? S : 1];
+  load_shared<NH, KB, JB, NP, NT2>(sh, img, cst);
+  if constexpr (VISSM_BWD2_PRIO == 1) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr (FZ) {
+    for (int i = threadIdx.x; i < NW2 * S * P; i += NT2) (&zls[0][0][0])[i] = 0.f;
+    for (int i = threadIdx.x; i < NW2 * S; i += NT2) (&zcar[0][0])[i] = 0.f;
+  }
+  for (int i = threadIdx.x; i < NW2 * S * DTH; i += NT2) (&dthl[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW2 * S * KP2; i += NT2) (&carry[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW2 * 2 * KP2 * QW2; i += NT2) (&dscr[0][0][0][0])[i] = 0.f;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW2 + w);
+  const int grp = __builtin_amdgcn_readfirstlane(item / a.n_chunks);
+  const int chn = __builtin_amdgcn_readfirstlane(item % a.n_chunks);
+  if (grp >= a.n_groups) return;
+  const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
+  const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
+  __bf16* const im0 = timg[w][0];  // I_0
+  __bf16* const im1 = timg[w][1];  // I_1, then dZ, then dA0
+  const unsigned* whp = reinterpret_cast<const unsigned*>(&sh.cst[NH * HP]);  // (mu, r) bf16 pairs
+
+  f4 dW[4][4], dWe[4], dWh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) dW[i][o] = f4{0.f, 0.f, 0.f, 0.f};
+    dWe[i] = f4{0.f, 0.f, 0.f, 0.f};
+    dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int fwc = 16 * NH + 4 * KB;
+  // d theta's ones operand, split by sample: B[k = 8g + jj][n = c] = 1 if position k belongs to the sample of
+  // column block n (columns 0-7: sample A = jj < 4, columns 8-15: sample B)
+  bf8 ones_ab;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) ones_ab[jj] = (__bf16)(((jj < 4) == (c < 8)) ? 1.f : 0.f);
+
+  const float ldl = (!FZ && lane < nb) ? dls[b_lo + lane] : 0.f;
+  float lt0 = 0.f, lt1 = 0.f, lis = 0.f;
+  if constexpr (FZ) {
+    if (lane < nb) {
+      const float* tp = fz.theta + static_cast<size_t>(b_lo + lane) * 3;
+      lt0 = tp[0];
+      lt1 = tp[1];
+      lis = __expf(-tp[2]);
+    }
+  }
+  const int m_start = (FZ && chn > 0) ? m_lo - PO : m_lo;
+  const int nu = a.k + P;  // u entries a unit reads (stride 1)
+  for (int m0 = m_start; m0 < m_hi; m0 += PO) {
+    const bool discard = FZ && m0 < m_lo;
+    const int nP = discard ? 0 : min(PO, m_hi - m0), t0 = m0;
+    const int nZ = FZ ? min(P, a.Lh - m0) : nP;
+    f4 dCa[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int bl = 0; bl < nb; bl += 2) {
+      fence();
+      const bool two = bl + 1 < nb;  // wave-uniform; else the second slot is a ghost
+      const int blv[2] = {bl, two ? bl + 1 : bl};
+      const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
+      // ---- inputs: the two u windows (and upstream-gradient windows), the shared C rows + each theta row
+      f4 X[2][4];
+      float fz_yp = 0.f, fz_bp = 0.f, fz_zc[2] = {0.f, 0.f};
+      {
+        float uv[2], gv[2] = {0.f, 0.f};
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float* ub = u + static_cast<size_t>(bv[cb]) * a.L;
+          uv[cb] = lane < nu ? ub[clampi(t0 + lane, a.L)] : 0.f;
+          if constexpr (!FZ) {
+            if (lane < P) gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.Lout + clampi(t0 + lane, a.Lout)];
+          }
+        }
+        if (!two) gv[1] = 0.f;
+        if constexpr (FZ) {
+          const int wo = min(max(m0 + c - 1, 0), fz.M - 1);
+          fz_yp = fz.obs[wo];
+          fz_bp = fz.bin[wo];
+        }
+        const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nZ)) * HP) + g;
+        f4 cr[4], tr[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          cr[rb] = crow[4 * rb];
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          uwin[w][cb][lane] = uv[cb];
+          if (lane < P) gwin[w][cb][lane] = gv[cb];
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
+        }
+        if constexpr (FZ) {
+          fz_zc[0] = zcar[w][blv[0]];
+          fz_zc[1] = zcar[w][blv[1]];
+        }
+      }
+      // ---- forward recompute of both samples (shared weight fragments)
+      u2 i0p[2][4];
+      float mu[2], rr[2];
+      {
+        f4 acc[2][4];
+        fence();
+        Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c), u_frag<NP>(uwin[w][1], 1, 0, g, c)};
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], X[cb][ob]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD_MED3>(acc[cb][rb][r]) : 0.f;
+        fence();
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (g == 3) X[cb][3][3] = 1.f;  // the ones row: bias of the hidden layer
+#pragma unroll
+          for (int ob = 0; ob < 4; ++ob) acc[cb][ob] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          Fr8<NP> xf[2] = {chain_frag<NP>(X[0], ks), chain_frag<NP>(X[1], ks)};
+#pragma unroll
+          for (int ob = 0; ob < 4; ++ob) {
+            const Fr8<NP> wf = wfrag(sh, ob * 2 + ks, lane);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, xf[cb], acc[cb][ob]);
+          }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          put_image<NP>(im0 + cb * P * HP, nullptr, X[cb], g, c);  // I_0 with its ones row
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) i0p[cb][rb] = u2{cvt2(X[cb][rb][0], X[cb][rb][1]), cvt2(X[cb][rb][2], X[cb][rb][3])};
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD_MED3>(acc[cb][rb][r]) : 0.f;
+        fence();
+        const int fh = 16 * NH + 4 * KB + 2 * JB;
+        f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          if (g == 3) X[cb][3][3] = 1.f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> wf = wfrag(sh, fh + ks, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) d[cb] = mm<NP>(wf, chain_frag<NP>(X[cb], ks), d[cb]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          mu[cb] = d[cb][0];
+          rr[cb] = d[cb][1];
+          put_image<NP>(im1 + cb * P * HP, nullptr, X[cb], g, c);  // I_1 (head input) with its ones row
+        }
+      }
+      // ---- head backward, per sample
+      const bool pv = c < nP;
+      float sig[2], gmu[2], gr[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        sig[cb] = softplus_fast(rr[cb]) + 1e-10f;
+        if constexpr (FZ) {
+          const float x = uwin[w][cb][c + a.k] * sig[cb] + mu[cb];
+          float xp = row_prev(x);
+          const float xn = row_next(x);
+          if (c == 0) xp = fz_zc[cb];
+          const int bl2 = blv[cb];
+          if (discard) {
+            if (lane == PO - 1 && (cb == 0 || two)) zcar[w][bl2] = x;
+            gmu[cb] = 0.f;
+            continue;
+          }
+          const float th0 = lane_f(lt0, bl2), th1 = lane_f(lt1, bl2), is = lane_f(lis, bl2);
+          const int t = m0 + c;
+          const float fh = (pv && t < fz.M) ? 1.f : 0.f;
+          const float ft = (pv && t >= 1) ? 1.f : 0.f;
+          const float bp = fz_bp * ft;
+          const float zt = fh * (xn - th1 * x - th0) * is;
+          const float zp = ft * (x - th1 * xp - th0) * is;
+          const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
+          gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
+          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __logf(sig[cb]) : 0.f;
+          if (g == 0) {
+            gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the rest of the unit reads
+            if (pv && (cb == 0 || two)) {
+              fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
+              zls[w][bl2][c] += lsg;
+            }
+          }
+          if (lane == PO - 1 && nP == PO && (cb == 0 || two)) zcar[w][bl2] = x;
+        } else {
+          gmu[cb] = pv ? gwin[w][cb][c] : 0.f;
+        }
+      }
+      if (discard) continue;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const float dl = FZ ? -fz.scale : lane_f(ldl, blv[cb]);
+        float dsig = gmu[cb] * uwin[w][cb][c + a.k];
+        if (pv && (cb == 0 || two) && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig[cb]);
+        gr[cb] = dsig * sigmoid_fast(rr[cb]);
+        if (g == 0) gsc[w][cb][c] = sig[cb];
+        // the head gradient G = (g_mu, g_r) at p = c into the I_1 image's padding rows 53, 54 (register (3, 1),
+        // (3, 2) of lane group 1; unit 49 in row 52 rewritten unchanged): dW_head = I_1 G^T then takes both
+        // operands from this one image, before the dZ image overwrites its slot
+        if (g == 1) {
+          const int off = timg_off(c, 4 * 3 + 1);
+          *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
+        }
+      }
+      fence();
+      // dW_head[h][o] += sum over both samples' positions of I_1[h][p] G[o][p] (K = 32): block 3 of the same
+      // fragments is the B operand (its columns 5, 6 are the G rows)
+      {
+        bf8 i1f[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) i1f[hb] = tr_frag2(im1, hb, g, c);
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mfma32(i1f[hb], i1f[3], dWh[hb]);
+      }
+      // dZ = (w~_mu g_mu + w~_r g_r) * elu'(I_1): one K = 16 MFMA per row block per sample
+      f4 D[2][4];
+      {
+        unsigned wvh[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) wvh[rb] = whp[16 * rb + c];
+        const bool g0 = g == 0;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const bf4 gf2 = __builtin_bit_cast(bf4, u2{cvt2(g0 ? gmu[cb] : 0.f, g0 ? gr[cb] : 0.f), 0u});
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const bf4 wa = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
+            D[cb][rb] = mfma16(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
+          }
+        }
+        fence();
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+          put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
+        }
+      }
+      fence();
+      // dX = W~ dZ (chain), both samples
+      f4 dX[2][4];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) dX[cb][ib] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        Fr8<NP> df[2] = {chain_frag<NP>(D[0], ks), chain_frag<NP>(D[1], ks)};
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          const Fr8<NP> wb = wfrag(sh, 8 * NH + ib * 2 + ks, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) dX[cb][ib] = mm<NP>(wb, df[cb], dX[cb][ib]);
+        }
+      }
+      fence();
+      // dW += I_0 dZ^T over both samples' positions (K = 32), from the two images
+      {
+        bf8 dzf[4];
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) dzf[ob] = tr_frag2(im1, ob, g, c);
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          const bf8 xa = tr_frag2(im0, ib, g, c);
+#pragma unroll
+          for (int ob = 0; ob < 4; ++ob) dW[ib][ob] = mfma32(xa, dzf[ob], dW[ib][ob]);
+        }
+      }
+      // dA0 = dX * elu'(I_0) (I_0 from the registers the forward left: the image's bf16 values)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const f4 x = {__builtin_bit_cast(float, i0p[cb][rb][0] << 16), __builtin_bit_cast(float, i0p[cb][rb][0] & 0xffff0000u),
+                        __builtin_bit_cast(float, i0p[cb][rb][1] << 16), __builtin_bit_cast(float, i0p[cb][rb][1] & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+        }
+      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p] per sample; the dC tile += dA0 of both
+      f4 dcn[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+      if constexpr (DU) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> wc = wfrag(sh, fwc + ks, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) dcn[cb] = mm<NP>(wc, chain_frag<NP>(D[cb], ks), dcn[cb]);
+        }
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);  // dA0 -> slot 1
+      if constexpr (DU) {
+        // dcon stores (rows j < KP2: lane groups 0, 1)
+        if (g < KP2 / 4) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dscr[w][cb][4 * g + r][c + 4 * g + r] = dcn[cb][r];
+        }
+      }
+      fence();
+      // dW_eps and d theta from dA0's position-contracted fragments (K = 32)
+      f4 dth4[4];
+      {
+        bf8 uaf;
+        {
+          const Fr4<NP> ua = ua_frag<NP>(uwin[w][0], 1, 0, g, c), ub = ua_frag<NP>(uwin[w][1], 1, 0, g, c);
+          uaf = cat8(ua.h, ub.h);
+        }
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) {
+          const bf8 ta = tr_frag2(im1, hb, g, c);
+          dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
+          dWe[hb] = mfma32(uaf, ta, dWe[hb]);
+        }
+      }
+      // per-sample d theta read-modify-writes: lane c = 0 (sample A) and c = 8 (sample B)
+      if (c == 0 || (c == 8 && two)) {
+        float* base = &dthl[w][c == 0 ? blv[0] : blv[1]][4 * g];
+        f4* dp[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb)
+          dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
+        f4 o[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
+      }
+      // du over local positions q in [0, nP + k) for both samples at once: lane = 32 cb + q
+      if constexpr (DU) {
+        fence();
+        const int cbq = lane >> 5, q = lane & 31;
+        const int lim = nP + a.k;
+        if (q < lim && (cbq == 0 || two)) {
+          const int qc = q < QW2 ? q : QW2 - 1;
+          float t[KP2];
+#pragma unroll
+          for (int j = 0; j < KP2; ++j) t[j] = dscr[w][cbq][j][qc];
+#pragma unroll
+          for (int w2 = 1; w2 < KP2; w2 *= 2)
+#pragma unroll
+            for (int j = 0; j + w2 < KP2; j += 2 * w2) t[j] += t[j + w2];
+          float v = t[0];
+          const int oq2 = q - a.k;
+          if (oq2 >= 0 && oq2 < nP) v += gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
+          const int blq = cbq ? blv[1] : blv[0];
+          if (q < a.k) v += carry[w][blq][q];
+          if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.L + t0 + q] = v;
+          else carry[w][blq][q - nP] = v;
+        }
+      }
+    }
+    // tile done: its dC over the group (both samples of every pair)
+    if (c < nP) {
+      const size_t row = (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
+      if (a.dc16) {
+        __bf16* dcs = reinterpret_cast<__bf16*>(dC_slab) + row;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = swz(16 * rb + 4 * g + r);
+            if (h < a.H) dcs[h] = static_cast<__bf16>(dCa[rb][r] * kLog2e);
+          }
+      } else {
+        float* dcs = dC_slab + row;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = swz(16 * rb + 4 * g + r);
+            if (h < a.H) dcs[h] = dCa[rb][r] * kLog2e;
+          }
+      }
+    }
+  }
+
+  if constexpr (FZ) {
+    if (lane < nb) {
+      float v = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < P; ++cc) v += zls[w][lane][cc];
+      fz.lsl[static_cast<size_t>(chn) * a.B + b_lo + lane] = v;
+    }
+  }
+  for (int bl = 0; bl < nb; ++bl) {
+    const int b = b_lo + bl;
+    if constexpr (DU) {
+      if (lane < a.k) {
+        const float v = carry[w][bl][lane];
+        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + lane] = v;
+        else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + lane] = v;
+      }
+    }
+    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
+  }
+
+  // weight-gradient partials of this work item (the layout of bwd_kernel's)
+  const int H = a.H;
+  const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
+  float* ws = dW_slab + static_cast<size_t>(item) * nW;
+#pragma unroll
+  for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 4 * g + r, h = swz(16 * hb + c);
+      if (j < a.k && h < H) ws[j * H + h] = dWe[hb][r] * kLog2e;
+    }
+  const int off_w = a.k * H, off_b = off_w + NH * H * H;
+#pragma unroll
+  for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hi = swz(16 * ib + 4 * g + r), ho = swz(16 * ob + c);
+        if (ho < H) {
+          if (hi < H) ws[off_w + hi * H + ho] = dW[ib][ob][r];
+          else if (hi == 63) ws[off_b + ho] = dW[ib][ob][r] * kLog2e;
+        }
+      }
+  for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;
+  const int off_h = off_b + 3 * NH * H;
+  const int oh = c - 5;
+  if (oh == 0 || oh == 1) {
+#pragma unroll
+    for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = swz(16 * hb + 4 * g + r);
+        if (h < H) ws[off_h + h * 2 + oh] = dWh[hb][r] * kLn2;
+        else if (h == 63) ws[off_h + 2 * H + oh] = dWh[hb][r];
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 struct Geom {
@@ -1552,6 +2071,12 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowPar
   }
 }
 
+// the two-sample backward covers the AR configurations' flow shape
+static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
+  return VISSM_BWD2 && d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
+         d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S && !g.dcb;
+}
+
 }  // namespace flow5
 
 using namespace flow5;
@@ -1678,7 +2203,15 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int pvar = du ? VISSM_PROF_FLOW_BWD_DU : VISSM_PROF_FLOW_BWD_NODU;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(pvar, st);
-  if (du)
+  if (bwd2_ok(d, g)) {
+    const dim3 grid2((g.n_items + NW2 - 1) / NW2);
+    if (du)
+      hipLaunchKernelGGL((bwd2_kernel<false, true>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig,
+                         ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, FzArgs{});
+    else
+      hipLaunchKernelGGL((bwd2_kernel<false, false>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig,
+                         ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, FzArgs{});
+  } else if (du)
     FLOW5_DISPATCH_T(bwd_kernel, false COMMA true, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
                      ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
                      ws.halo, FzArgs{});
@@ -1759,9 +2292,14 @@ int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(VISSM_PROF_FLOW_FUSED, st);
-  FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,
-                    static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst, du,
-                    ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
+  if (bwd2_ok(d, g))
+    hipLaunchKernelGGL((bwd2_kernel<true, true>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u, ws.Cp,
+                       ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst,
+                       du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
+  else
+    FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,
+                      static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst, du,
+                      ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
   VISSM_CHECK_LAUNCH("flow5_fused");
   prof_end(VISSM_PROF_FLOW_FUSED, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
