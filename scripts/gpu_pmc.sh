@@ -12,6 +12,6 @@ i=0
 for SET in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   echo "== pass $i"
-  cd /tmp && timeout -k 10 600 rocprofv3 --pmc $SET --kernel-trace --stats -T --kernel-include-regex "bwd_kernel|fwd_kernel" -d "$OUT/${TAG}_$i" -o pmc --output-format csv -- python "$ROOT/scripts/flow_bench.py" --B $B --only $IMPL --rounds 2 ${EXTRA} > "$OUT/${TAG}_$i.log" 2>&1 || { tail -20 "$OUT/${TAG}_$i.log"; exit 3; }
+  cd /tmp && timeout -k 10 600 rocprofv3 --pmc $SET --kernel-trace --stats -T --kernel-include-regex "bwd|fwd_kernel" -d "$OUT/${TAG}_$i" -o pmc --output-format csv -- python "$ROOT/scripts/flow_bench.py" --B $B --only $IMPL --rounds 2 ${EXTRA} > "$OUT/${TAG}_$i.log" 2>&1 || { tail -20 "$OUT/${TAG}_$i.log"; exit 3; }
 done
 cd "$ROOT" && python scripts/pmc_summary.py "$OUT/${TAG}_1" "$OUT/${TAG}_2" "$OUT/${TAG}_3" "$OUT/${TAG}_4"

@@ -56,18 +56,21 @@ def _post_stats(theta):
 #    float32 oracle's own drift from the float64 trajectory + 2e-5 absolute, per-sample ELBO within 1e-4
 #    (or 10x the float32 oracle's error where the step's ELBO is an ill-conditioned cancellation);
 #  * bf16x2f at the AR-cfg length (BASELINE configs[1]'s window, where that precision holds the ELBO to
-#    1e-4: tests/test_gpu_config_parity.py): ELBO within 1e-4, posterior mean / sd within 2e-3 absolute
-#    (its backward products are bf16: the gradient, and so the Adamax trajectory, is bf16-accurate)
-TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance)
-    "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4),
-    "bf16x2f": (20, 5000, 8, 5000, 0.0, 2e-3, 1e-4),
+#    1e-4: tests/test_gpu_config_parity.py): the first step's ELBO (same parameters on both sides) within
+#    1e-4; after it the parameters differ by the bf16 gradients' Adamax steps (its backward products are
+#    bf16, and Adamax's normalised steps pass a gradient's rounding straight into the parameters: measured
+#    ELBO 1.5e-3 and posterior mean 6e-4 apart after 10 steps), so ELBO within 5e-3 and posterior mean / sd
+#    within 5e-3 absolute; that the bf16 path trains to the same posterior is test (b) at bf16
+TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance at step 0, after)
+    "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4, 1e-4),
+    "bf16x2f": (20, 5000, 8, 5000, 0.0, 5e-3, 1e-4, 5e-3),
 }
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16x2f"])
 def test_ar_posterior_trajectory_matches_oracle(prec):
     K = 20
-    p, M, k, T, mult, floor, elbo_tol = TRAJ[prec]
+    p, M, k, T, mult, floor, elbo_tol0, elbo_tol = TRAJ[prec]
     model = build_model("ar", p, M, k, 3, 50, 3, 10, DEV, T=T, precision=PREC[prec], impute=1 if M < T else 5,
                         condition=True)
     md = model.mdef
@@ -125,7 +128,7 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
         assert np.isfinite(eg).all() and np.isfinite(mg).all()
         assert dgm <= mult * d32m + floor, (step, dgm, d32m)
         assert dgs <= mult * d32s + floor, (step, dgs, d32s)
-        assert erel <= max(elbo_tol, 10 * erel32), (step, erel, erel32)
+        assert erel <= max(elbo_tol0 if step == 0 else elbo_tol, 10 * erel32), (step, erel, erel32)
         worst = {"dmean": max(worst["dmean"], dgm), "dsd": max(worst["dsd"], dgs), "elbo": max(worst["elbo"], erel)}
     print("worst over the trajectory:", worst)
     # the trajectory moved the posterior by more than the tolerance (the comparison is not vacuous)
@@ -140,13 +143,16 @@ RECOVERY_BAND = {"theta0": (5.0, 0.5), "theta1": (0.5, 0.05), "e^theta2": (3.0, 
 RECOVERY_SD_MAX = (0.5, 0.05, 0.15)
 
 
-def test_ar_posterior_recovers_generating_theta():
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_ar_posterior_recovers_generating_theta(prec):
+    """fp32 (the reference's arithmetic) and bf16 (the benchmark's flow products) both train to the posterior
+    the data imply."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import ar_recovery
     cwd = os.getcwd()
     os.chdir(ROOT)
     try:
-        _, recs = ar_recovery.run(steps=RECOVERY_STEPS, every=max(1000, RECOVERY_STEPS // 10), precision="fp32")
+        _, recs = ar_recovery.run(steps=RECOVERY_STEPS, every=max(1000, RECOVERY_STEPS // 10), precision=prec)
     finally:
         os.chdir(cwd)
     m = recs[-1]["mean"]

@@ -30,8 +30,11 @@
 //   * grid decomposition, carries, halo and fixed-order partial slabs follow
 //     flow_v4.hip (sample groups x t-chunks; the backward walks tiles outer / samples
 //     inner so the window-shared dC tile is summed over the group in accumulators).
-// Supported: n_hidden = 1 without BN, H <= 63, k <= 64 (the AR configurations);
-// other shapes run on flow_v4 (exact fp32).
+// Supported (flow5_supports): H <= 50, k <= 64; bf16 with one hidden layer (AR) or three hidden layers with
+// the BN affine folded into the weights (LV / SV / FHN heads: bwd_kernel<3, ...>, one wave per SIMD -- its
+// three dW accumulator sets take 192 of the 512 registers), bf16x3 / bf16x2 with one hidden layer and k <= 32.
+// The AR configurations' backward (bf16, one hidden layer, k <= 8, stride 1, one window) runs bwd2_kernel:
+// two samples per unit, see below.  Everything else runs on flow_v4 / flow_v2 (exact fp32).
 #include "common.hpp"
 
 #include <cstdlib>
@@ -1420,6 +1423,19 @@ constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 #ifndef VISSM_BWD2
 #define VISSM_BWD2 1
 #endif
+#ifndef VISSM_BWD2_FENCE
+#define VISSM_BWD2_FENCE 2  // compiler fences between the unit's phases: 1 always, 0 never, 2 in the fused (FZ)
+                            // variant only (A/B, AR-cfg launches: middle flows 23.3 -> 22.4 ms without them, the
+                            // fused one 26.8 -> 28.2, the first flow unchanged)
+#endif
+#ifndef VISSM_BWD2_MED3
+#define VISSM_BWD2_MED3 1  // the recompute's ELU select as v_med3 (one instruction fewer per element): 93.3 -> 91.4 ms
+                           // per AR-cfg step (A/B); in the one-sample kernel it measured slower
+#endif
+template <bool FZ>
+__device__ __forceinline__ void fence2() {
+  if constexpr (VISSM_BWD2_FENCE == 1 || (VISSM_BWD2_FENCE == 2 && FZ)) fence();
+}
 #ifndef VISSM_BWD2_PRIO
 #define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
 #endif
@@ -1512,7 +1528,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
     for (int bl = 0; bl < nb; bl += 2) {
-      fence();
+      fence2<FZ>();
       const bool two = bl + 1 < nb;  // wave-uniform; else the second slot is a ghost
       const int blv[2] = {bl, two ? bl + 1 : bl};
       const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
@@ -1561,7 +1577,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       float mu[2], rr[2];
       {
         f4 acc[2][4];
-        fence();
+        fence2<FZ>();
         Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c), u_frag<NP>(uwin[w][1], 1, 0, g, c)};
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
@@ -1574,8 +1590,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD_MED3>(acc[cb][rb][r]) : 0.f;
-        fence();
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2_MED3>(acc[cb][rb][r]) : 0.f;
+        fence2<FZ>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           if (g == 3) X[cb][3][3] = 1.f;  // the ones row: bias of the hidden layer
@@ -1603,8 +1619,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD_MED3>(acc[cb][rb][r]) : 0.f;
-        fence();
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2_MED3>(acc[cb][rb][r]) : 0.f;
+        fence2<FZ>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -1678,7 +1694,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
         }
       }
-      fence();
+      fence2<FZ>();
       // dW_head[h][o] += sum over both samples' positions of I_1[h][p] G[o][p] (K = 32): block 3 of the same
       // fragments is the B operand (its columns 5, 6 are the G rows)
       {
@@ -1704,7 +1720,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             D[cb][rb] = mfma16(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
           }
         }
-        fence();
+        fence2<FZ>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
@@ -1714,7 +1730,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
         }
       }
-      fence();
+      fence2<FZ>();
       // dX = W~ dZ (chain), both samples
       f4 dX[2][4];
 #pragma unroll
@@ -1731,7 +1747,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int cb = 0; cb < 2; ++cb) dX[cb][ib] = mm<NP>(wb, df[cb], dX[cb][ib]);
         }
       }
-      fence();
+      fence2<FZ>();
       // dW += I_0 dZ^T over both samples' positions (K = 32), from the two images
       {
         bf8 dzf[4];
@@ -1780,7 +1796,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             for (int r = 0; r < 4; ++r) dscr[w][cb][4 * g + r][c + 4 * g + r] = dcn[cb][r];
         }
       }
-      fence();
+      fence2<FZ>();
       // dW_eps and d theta from dA0's position-contracted fragments (K = 32)
       f4 dth4[4];
       {
@@ -1811,7 +1827,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       // du over local positions q in [0, nP + k) for both samples at once: lane = 32 cb + q
       if constexpr (DU) {
-        fence();
+        fence2<FZ>();
         const int cbq = lane >> 5, q = lane & 31;
         const int lim = nP + a.k;
         if (q < lim && (cbq == 0 || two)) {
