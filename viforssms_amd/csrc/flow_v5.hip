@@ -1432,6 +1432,11 @@ constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 #define VISSM_BWD2_MED3 1  // the recompute's ELU select as v_med3 (one instruction fewer per element): 93.3 -> 91.4 ms
                            // per AR-cfg step (A/B); in the one-sample kernel it measured slower
 #endif
+#ifndef VISSM_BWD2_FZ_BRANCH
+#define VISSM_BWD2_FZ_BRANCH 0  // 0: a t-chunk's look-back tile (fused variant) runs the whole unit with every
+                                // gradient zero (nP = 0 masks them) instead of branching out after the recompute:
+                                // the branch split the unit into basic blocks the scheduler cannot interleave across
+#endif
 template <bool FZ>
 __device__ __forceinline__ void fence2() {
   if constexpr (VISSM_BWD2_FENCE == 1 || (VISSM_BWD2_FENCE == 2 && FZ)) fence();
@@ -1651,7 +1656,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           const float xn = row_next(x);
           if (c == 0) xp = fz_zc[cb];
           const int bl2 = blv[cb];
-          if (discard) {
+          if (VISSM_BWD2_FZ_BRANCH && discard) {
             if (lane == PO - 1 && (cb == 0 || two)) zcar[w][bl2] = x;
             gmu[cb] = 0.f;
             continue;
@@ -1673,12 +1678,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
               zls[w][bl2][c] += lsg;
             }
           }
-          if (lane == PO - 1 && nP == PO && (cb == 0 || two)) zcar[w][bl2] = x;
+          if (lane == PO - 1 && (nP == PO || discard) && (cb == 0 || two)) zcar[w][bl2] = x;
         } else {
           gmu[cb] = pv ? gwin[w][cb][c] : 0.f;
         }
       }
-      if (discard) continue;
+      if (VISSM_BWD2_FZ_BRANCH && discard) continue;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const float dl = FZ ? -fz.scale : lane_f(ldl, blv[cb]);
