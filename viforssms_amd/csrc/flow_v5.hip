@@ -1939,6 +1939,595 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 }
 
 // ---------------------------------------------------------------------------
+// forward kernel, two samples per unit ("fwd2"): the AR configurations' shape (one hidden layer, bf16, k <= 16,
+// stride 1, one window).  Pairs of samples outer, tiles inner: the pair's two chains run interleaved in one
+// wave and share the tile's C rows and every weight fragment (register-resident with VISSM_FWD2_REGW).
+// ---------------------------------------------------------------------------
+#ifndef VISSM_FWD2
+#define VISSM_FWD2 1
+#endif
+#ifndef VISSM_FWD2_REGW
+#define VISSM_FWD2_REGW 1
+#endif
+#ifndef VISSM_FWD2_OCC
+#define VISSM_FWD2_OCC 2
+#endif
+__global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const float* __restrict__ u,
+                                                                  const float* __restrict__ C,
+                                                                  const float* __restrict__ tht,
+                                                                  const bf8* __restrict__ img,
+                                                                  const float* __restrict__ cst,
+                                                                  float* __restrict__ u_next,
+                                                                  float* __restrict__ ls_slab) {
+  constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
+  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ float uwin[NW][2][64];
+  load_shared(sh, img, cst);
+  if constexpr (VISSM_FWD_PRIO == 3) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
+    if (r == 1) __builtin_amdgcn_s_setprio(1);
+    else if (r == 2) __builtin_amdgcn_s_setprio(2);
+    else if (r == 3) __builtin_amdgcn_s_setprio(3);
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);
+  if (item >= a.n_items) return;
+  const int grp = item / a.n_chunks, ch = item % a.n_chunks;
+  const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
+  const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
+  constexpr int NWR = VISSM_FWD2_REGW ? 8 * NH + 4 * KB + 2 : 1;
+  bf8 wr[NWR];
+  if constexpr (VISSM_FWD2_REGW) {
+#pragma unroll
+    for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
+#pragma unroll
+    for (int i = 0; i < 4 * KB; ++i) wr[8 * NH + i] = sh.img[16 * NH + i][0][lane];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
+  }
+  // fragment f of the shared image, or its register copy (index i)
+  auto W = [&](int f, int i) -> bf8 {
+    if constexpr (VISSM_FWD2_REGW) return wr[i];
+    else return sh.img[f][0][lane];
+  };
+  const int nu = a.k + P;
+  for (int bl = 0; bl < nb; bl += 2) {
+    const bool two = bl + 1 < nb;
+    const int bv[2] = {b_lo + bl, b_lo + (two ? bl + 1 : bl)};
+    float ls[2] = {0.f, 0.f};
+    for (int m0 = m_lo; m0 < m_hi; m0 += P) {
+      const int nP = min(P, m_hi - m0), t0 = m0;
+      f4 X[2][4];
+      {
+        float uv[2];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) uv[cb] = lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane, a.L)] : 0.f;
+        const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
+        f4 cr[4], tr[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          cr[rb] = crow[4 * rb];
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          uwin[w][cb][lane] = uv[cb];
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
+        }
+      }
+      f4 acc[2][4];
+      {
+        const bf8 uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c).h, u_frag<NP>(uwin[w][1], 1, 0, g, c).h};
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const bf8 wf = W(16 * NH + ob, 8 * NH + ob);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mfma32(wf, uf[cb], X[cb][ob]);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+        if (g == 3) X[cb][3][3] = 1.f;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) acc[cb][ob] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf8 xf[2] = {chain_frag<NP>(X[0], ks).h, chain_frag<NP>(X[1], ks).h};
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const bf8 wf = W(ob * 2 + ks, ob * 2 + ks);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mfma32(wf, xf[cb], acc[cb][ob]);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+        if (g == 3) X[cb][3][3] = 1.f;
+      }
+      const int fh = 16 * NH + 4 * KB + 2 * JB;
+      f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf8 wf = W(fh + ks, 8 * NH + 4 * KB + ks);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) d[cb] = mfma32(wf, chain_frag<NP>(X[cb], ks).h, d[cb]);
+      }
+      if (g == 0 && c < nP) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (cb == 1 && !two) break;
+          const float sg = softplus_fast(d[cb][1]) + 1e-10f;
+          const int o = t0 + c;
+          u_next[static_cast<size_t>(bv[cb]) * a.Lout + o] = uwin[w][cb][c + a.k] * sg + d[cb][0];
+          if (o >= a.Lout - a.n_logsig) ls[cb] += logf(sg);
+        }
+      }
+    }
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const float v = wave_sum(ls[cb]);
+      if (lane == 0 && (cb == 0 || two)) ls_slab[static_cast<size_t>(ch) * a.B + bv[cb]] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward kernel for three hidden layers (LV / SV / FHN heads, BN affine folded), two samples per unit
+// ("bwd2n").  The one-sample kernel above holds dW for three layers (192 registers) and runs one wave per
+// SIMD with nothing to cover its latencies (round-3 counters: half of a wave's cycles parked at s_waitcnt,
+// profiles/r03/bwd_nh3_counters_lv_B4096.txt).  Here the wave interleaves two samples' chains as bwd2_kernel
+// does, with the position contractions at K = 32 over the pair; the hidden activations I_0 .. I_3 stay in
+// registers as bf16 pairs (what the one-sample kernel read back from its images) and each is written into the
+// wave's image slot 0 only when its weight gradient is formed, next to D_l in slot 1, so two 32-row image
+// slots per wave suffice (the one-sample kernel kept four 16-row slots).  k <= 32, one window.
+// ---------------------------------------------------------------------------
+constexpr int NW3 = 4;
+constexpr int NT3 = 64 * NW3;
+#ifndef VISSM_BWD2N
+#define VISSM_BWD2N 1
+#endif
+#ifndef VISSM_BWD2N_MED3
+#define VISSM_BWD2N_MED3 1
+#endif
+
+__device__ __forceinline__ void put_pairs(__bf16* img, const u2 (&v)[4], int g, int c) {
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) *reinterpret_cast<u2*>(img + timg_off(c, 4 * rb + g)) = v[rb];
+}
+__device__ __forceinline__ f4 unpack_pair(u2 v) {
+  return f4{__builtin_bit_cast(float, v[0] << 16), __builtin_bit_cast(float, v[0] & 0xffff0000u),
+            __builtin_bit_cast(float, v[1] << 16), __builtin_bit_cast(float, v[1] & 0xffff0000u)};
+}
+
+template <int JB, bool S2, bool DU>
+__global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+                                                       const float* __restrict__ tht, const float* __restrict__ gout,
+                                                       const float* __restrict__ dls, const bf8* __restrict__ img,
+                                                       const float* __restrict__ cst, float* __restrict__ du,
+                                                       float* __restrict__ dC_slab, float* __restrict__ dth_slab,
+                                                       float* __restrict__ dW_slab, float* __restrict__ halo) {
+  constexpr int NH = 3, KB = (JB + 1) / 2, NP = 1;
+  static_assert(KB == 1, "k <= 32");
+  constexpr int s = S2 ? 2 : 1;
+  constexpr int KP = 16 * JB;
+  __shared__ Shared<NH, KB, JB, NP> sh;
+  __shared__ __bf16 timg[NW3][2][2 * P * HP];  // slot 0: I_l, slot 1: D_l, then dA0
+  __shared__ float dthl[NW3][S][DTH];
+  __shared__ __attribute__((aligned(16))) float dths[NW3][4];
+  __shared__ float carry[NW3][S][KP];
+  __shared__ float gsc[NW3][2][2][P];  // per sample: sigma, the even outputs' pass-through gradient (stride 2)
+  __shared__ float uwin[NW3][2][64];
+  __shared__ float gwin[NW3][2][s * P];
+  __shared__ float dscr[NW3][2][KP][P];  // dcon[j][p]
+  load_shared<NH, KB, JB, NP, NT3>(sh, img, cst);
+  for (int i = threadIdx.x; i < NW3 * S * DTH; i += NT3) (&dthl[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW3 * S * KP; i += NT3) (&carry[0][0][0])[i] = 0.f;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW3 + w);
+  const int grp = __builtin_amdgcn_readfirstlane(item / a.n_chunks);
+  const int chn = __builtin_amdgcn_readfirstlane(item % a.n_chunks);
+  if (grp >= a.n_groups) return;
+  const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
+  const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
+  __bf16* const im0 = timg[w][0];
+  __bf16* const im1 = timg[w][1];
+  const unsigned* whp = reinterpret_cast<const unsigned*>(&sh.cst[NH * HP]);
+
+  f4 dW[NH][4][4], dWe[JB][4], dWh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int l = 0; l < NH; ++l)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) dW[l][i][o] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb) dWe[jb][i] = f4{0.f, 0.f, 0.f, 0.f};
+    dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int fwc = 16 * NH + 4 * KB, fh = 16 * NH + 4 * KB + 2 * JB;
+  bf8 ones_ab;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) ones_ab[jj] = (__bf16)(((jj < 4) == (c < 8)) ? 1.f : 0.f);
+  const float ldl = lane < nb ? dls[b_lo + lane] : 0.f;
+  const int nu = s * P + a.k;
+  for (int m0 = m_lo; m0 < m_hi; m0 += P) {
+    const int nP = min(P, m_hi - m0), t0 = s * m0, fin = s * nP;
+    f4 dCa[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int bl = 0; bl < nb; bl += 2) {
+      fence();
+      const bool two = bl + 1 < nb;
+      const int blv[2] = {bl, two ? bl + 1 : bl};
+      const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
+      f4 X[2][4];
+      {
+        float uv[2], gv[2] = {0.f, 0.f};
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          uv[cb] = lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane, a.L)] : 0.f;
+          if (lane < s * P) {
+            const int o = t0 + lane;
+            gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.Lout + clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
+          }
+        }
+        if (!two) gv[1] = 0.f;
+        const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
+        f4 cr[4], tr[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          cr[rb] = crow[4 * rb];
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          uwin[w][cb][lane] = uv[cb];
+          if (lane < s * P) gwin[w][cb][lane] = gv[cb];
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
+        }
+      }
+      // ---- forward recompute of both samples; I_0 .. I_NH kept as bf16 pairs (with the ones row)
+      u2 ip[NH + 1][2][4];
+      float mu[2], rr[2];
+      {
+        f4 acc[2][4];
+        fence();
+        const Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], s, 0, g, c), u_frag<NP>(uwin[w][1], s, 0, g, c)};
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], X[cb][ob]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2N_MED3>(acc[cb][rb][r]) : 0.f;
+#pragma unroll
+        for (int l = 0; l < NH; ++l) {
+          fence();
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            if (g == 3) X[cb][3][3] = 1.f;
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+              ip[l][cb][rb] = u2{cvt2(X[cb][rb][0], X[cb][rb][1]), cvt2(X[cb][rb][2], X[cb][rb][3])};
+              acc[cb][rb] = f4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const Fr8<NP> xf[2] = {chain_frag<NP>(X[0], ks), chain_frag<NP>(X[1], ks)};
+#pragma unroll
+            for (int ob = 0; ob < 4; ++ob) {
+              const Fr8<NP> wf = wfrag(sh, l * 8 + ob * 2 + ks, lane);
+#pragma unroll
+              for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, xf[cb], acc[cb][ob]);
+            }
+          }
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2N_MED3>(acc[cb][rb][r]) : 0.f;
+        }
+        fence();
+        f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (g == 3) X[cb][3][3] = 1.f;
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+            ip[NH][cb][rb] = u2{cvt2(X[cb][rb][0], X[cb][rb][1]), cvt2(X[cb][rb][2], X[cb][rb][3])};
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> wf = wfrag(sh, fh + ks, lane);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) d[cb] = mm<NP>(wf, chain_frag<NP>(X[cb], ks), d[cb]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          mu[cb] = d[cb][0];
+          rr[cb] = d[cb][1];
+        }
+      }
+      // ---- head backward per sample; G rides in the I_NH image's padding rows 53, 54
+      const bool pv = c < nP;
+      const int oq = s * c + (s - 1);
+      float gmu[2], gr[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const float sig = softplus_fast(rr[cb]) + 1e-10f;
+        gmu[cb] = pv ? gwin[w][cb][oq] : 0.f;
+        float dsig = gmu[cb] * uwin[w][cb][oq + a.k];
+        if (pv && (cb == 0 || two) && t0 + oq >= a.Lout - a.n_logsig) dsig += lane_f(ldl, blv[cb]) * rcp_f(sig);
+        gr[cb] = dsig * sigmoid_fast(rr[cb]);
+        if (g == 0) {
+          gsc[w][cb][0][c] = sig;
+          if constexpr (S2) gsc[w][cb][1][c] = pv ? gwin[w][cb][2 * c] : 0.f;
+        }
+        u2 v3[4] = {ip[NH][cb][0], ip[NH][cb][1], ip[NH][cb][2], ip[NH][cb][3]};
+        if (g == 1) v3[3] = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
+        put_pairs(im0 + cb * P * HP, v3, g, c);
+      }
+      fence();
+      {
+        bf8 i1f[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) i1f[hb] = tr_frag2(im0, hb, g, c);
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mfma32(i1f[hb], i1f[3], dWh[hb]);
+      }
+      f4 D[2][4];
+      {
+        unsigned wvh[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) wvh[rb] = whp[16 * rb + c];
+        const bool g0 = g == 0;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const bf4 gf2 = __builtin_bit_cast(bf4, u2{cvt2(g0 ? gmu[cb] : 0.f, g0 ? gr[cb] : 0.f), 0u});
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const bf4 wa = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
+            D[cb][rb] = mfma16(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
+          }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+      }
+      // ---- hidden layers, top down: D = dZ_l; dW_l += I_l D^T; D <- (W_l D) * elu'(I_l)
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        fence();
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
+          put_pairs(im0 + cb * P * HP, ip[l][cb], g, c);
+        }
+        f4 dX[2][4];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int ib = 0; ib < 4; ++ib) dX[cb][ib] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> df[2] = {chain_frag<NP>(D[0], ks), chain_frag<NP>(D[1], ks)};
+#pragma unroll
+          for (int ib = 0; ib < 4; ++ib) {
+            const Fr8<NP> wb = wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) dX[cb][ib] = mm<NP>(wb, df[cb], dX[cb][ib]);
+          }
+        }
+        fence();
+        {
+          bf8 dzf[4];
+#pragma unroll
+          for (int ob = 0; ob < 4; ++ob) dzf[ob] = tr_frag2(im1, ob, g, c);
+#pragma unroll
+          for (int ib = 0; ib < 4; ++ib) {
+            const bf8 xa = tr_frag2(im0, ib, g, c);
+#pragma unroll
+            for (int ob = 0; ob < 4; ++ob) dW[l][ib][ob] = mfma32(xa, dzf[ob], dW[l][ib][ob]);
+          }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const f4 x = unpack_pair(ip[l][cb][rb]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+          }
+      }
+      // ---- D = dA0: dC tile, dcon, dW_eps, d theta
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
+      fence();
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
+      if constexpr (DU) {
+        f4 dcn[2][JB];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb) dcn[cb][jb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const Fr8<NP> df[2] = {chain_frag<NP>(D[0], ks), chain_frag<NP>(D[1], ks)};
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb) {
+            const Fr8<NP> wc = wfrag(sh, fwc + jb * 2 + ks, lane);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) dcn[cb][jb] = mm<NP>(wc, df[cb], dcn[cb][jb]);
+          }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = 16 * jb + 4 * g + r;
+              if (j < a.k) dscr[w][cb][j][c] = dcn[cb][jb][r];
+            }
+      }
+      fence();
+      f4 dth4[4];
+      {
+        bf8 uaf[JB];
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb)
+          uaf[jb] = cat8(ua_frag<NP>(uwin[w][0], s, jb, g, c).h, ua_frag<NP>(uwin[w][1], s, jb, g, c).h);
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) {
+          const bf8 ta = tr_frag2(im1, hb, g, c);
+          dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mfma32(uaf[jb], ta, dWe[jb][hb]);
+        }
+      }
+      if (c == 0 || (c == 8 && two)) {
+        float* base = &dthl[w][c == 0 ? blv[0] : blv[1]][4 * g];
+        f4* dp[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb)
+          dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
+        f4 o[4];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
+      }
+      // ---- du over local positions q in [0, fin + k) of each sample: transposed conv + pass-through + carry
+      if constexpr (DU) {
+        fence();
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (cb == 1 && !two) break;
+          const int q = lane;
+          if (q < fin + a.k) {
+            float v = 0.f;
+            for (int j = 0; j < a.k; ++j) {
+              const int t = q - j;
+              const int pp = S2 ? (t >> 1) : t;
+              const bool ok = t >= 0 && pp < nP && (!S2 || !(t & 1));
+              const float x = dscr[w][cb][j][pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp)];
+              v += ok ? x : 0.f;
+            }
+            const int oq2 = q - a.k;
+            if (oq2 >= 0 && oq2 < fin) {
+              if constexpr (S2) v += (oq2 & 1) ? gwin[w][cb][oq2] * gsc[w][cb][0][oq2 >> 1] : gsc[w][cb][1][oq2 >> 1];
+              else v += gwin[w][cb][oq2] * gsc[w][cb][0][oq2];
+            }
+            const int blq = blv[cb];
+            if (q < a.k) v += carry[w][blq][q];
+            if (q < fin) du[static_cast<size_t>(bv[cb]) * a.L + t0 + q] = v;
+            else carry[w][blq][q - fin] = v;
+          }
+        }
+      }
+    }
+    if (c < nP) {
+      const size_t row = (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
+      float* dcs = dC_slab + row;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = swz(16 * rb + 4 * g + r);
+          if (h < a.H) {
+            if (a.dc16) reinterpret_cast<__bf16*>(dC_slab)[row + h] = static_cast<__bf16>(dCa[rb][r] * kLog2e);
+            else dcs[h] = dCa[rb][r] * kLog2e;
+          }
+        }
+    }
+  }
+  for (int bl = 0; bl < nb; ++bl) {
+    const int b = b_lo + bl;
+    if constexpr (DU) {
+      for (int q = lane; q < a.k; q += 64) {
+        const float v = carry[w][bl][q];
+        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
+        else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
+      }
+    }
+    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
+  }
+  const int H = a.H;
+  const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
+  float* ws = dW_slab + static_cast<size_t>(item) * nW;
+#pragma unroll
+  for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+    for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * jb + 4 * g + r, h = swz(16 * hb + c);
+        if (j < a.k && h < H) ws[j * H + h] = dWe[jb][hb][r] * kLog2e;
+      }
+  const int off_w = a.k * H, off_b = off_w + NH * H * H;
+#pragma unroll
+  for (int l = 0; l < NH; ++l)
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hi = swz(16 * ib + 4 * g + r), ho = swz(16 * ob + c);
+          if (ho < H) {
+            if (hi < H) ws[off_w + (l * H + hi) * H + ho] = dW[l][ib][ob][r];
+            else if (hi == 63) ws[off_b + l * H + ho] = dW[l][ib][ob][r] * kLog2e;
+          }
+        }
+  for (int i = lane; i < 2 * NH * H; i += 64) ws[off_b + NH * H + i] = 0.f;
+  const int off_h = off_b + 3 * NH * H;
+  const int oh = c - 5;
+  if (oh == 0 || oh == 1) {
+#pragma unroll
+    for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = swz(16 * hb + 4 * g + r);
+        if (h < H) ws[off_h + h * 2 + oh] = dWh[hb][r] * kLn2;
+        else if (h == 63) ws[off_h + 2 * H + oh] = dWh[hb][r];
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 struct Geom {
@@ -2098,6 +2687,18 @@ static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
          d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S && !g.dcb;
 }
 
+// the three-hidden-layer two-sample backward: LV / FHN heads (k <= 32), one window
+static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
+  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 && d->k <= 32 && d->H <= kMaxH &&
+         d->n_win == 1 && g.S == S && !g.dcb;
+}
+
+// the two-sample forward covers the AR configurations' flow shape
+static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
+  return VISSM_FWD2 && d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
+         d->k <= 16 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
+}
+
 }  // namespace flow5
 
 using namespace flow5;
@@ -2192,7 +2793,9 @@ int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  if (np_of(d) == 2) {
+  if (fwd2_ok(d, g)) {
+    hipLaunchKernelGGL(fwd2_kernel, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, ws.ls_slab);
+  } else if (np_of(d) == 2) {
     if (jb_of(d->k) == 1)
       hipLaunchKernelGGL((fwd_kernel<1, 1, 1, 2>), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst, u_next,
                          ws.ls_slab);
@@ -2224,7 +2827,21 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int pvar = du ? VISSM_PROF_FLOW_BWD_DU : VISSM_PROF_FLOW_BWD_NODU;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(pvar, st);
-  if (bwd2_ok(d, g)) {
+  if (bwd2n_ok(d, g)) {
+    const dim3 grid3((g.n_items + NW3 - 1) / NW3);
+#define BWD2N_LAUNCH(JB_, S2_, DU_)                                                                              \
+  hipLaunchKernelGGL((bwd2n_kernel<JB_, S2_, DU_>), grid3, dim3(NT3), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig, \
+                     ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo)
+    const int jb = jb_of(d->k);
+    if (d->stride2) {
+      if (jb == 1) { if (du) BWD2N_LAUNCH(1, true, true); else BWD2N_LAUNCH(1, true, false); }
+      else { if (du) BWD2N_LAUNCH(2, true, true); else BWD2N_LAUNCH(2, true, false); }
+    } else {
+      if (jb == 1) { if (du) BWD2N_LAUNCH(1, false, true); else BWD2N_LAUNCH(1, false, false); }
+      else { if (du) BWD2N_LAUNCH(2, false, true); else BWD2N_LAUNCH(2, false, false); }
+    }
+#undef BWD2N_LAUNCH
+  } else if (bwd2_ok(d, g)) {
     const dim3 grid2((g.n_items + NW2 - 1) / NW2);
     if (du)
       hipLaunchKernelGGL((bwd2_kernel<false, true>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig,
