@@ -21,7 +21,7 @@ cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof" 
 tail -1 "$OUT/prof.log"
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"; date
-  cd /tmp && timeout -k 10 900 rocprofv3 --pmc $C --kernel-trace --stats -T --kernel-include-regex "bwd_kernel" -d "$OUT/pmc_$C" -o pmc --output-format csv -- python "$ROOT/bench.py" --steps 1 --warmup 0 --cpu-baseline off --parity-line off $BENCH_ARGS > "$OUT/pmc_$C.log" 2>&1 || { tail -20 "$OUT/pmc_$C.log"; exit 5; }
+  cd /tmp && timeout -k 10 900 rocprofv3 --pmc $C --kernel-trace --stats -T --kernel-include-regex "bwd" -d "$OUT/pmc_$C" -o pmc --output-format csv -- python "$ROOT/bench.py" --steps 1 --warmup 0 --cpu-baseline off --parity-line off $BENCH_ARGS > "$OUT/pmc_$C.log" 2>&1 || { tail -20 "$OUT/pmc_$C.log"; exit 5; }
 done
 date
 cd "$ROOT" && python scripts/traffic_from_pmc.py ${PREC:-bf16} 65536 5000 8

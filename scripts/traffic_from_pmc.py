@@ -15,7 +15,7 @@ def per_launch(counter):
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{counter}", "**", "*counter_collection.csv"),
                        recursive=True):
         for row in csv.DictReader(open(f)):
-            if row["Kernel_Name"].startswith("bwd_kernel") and row["Counter_Name"] == counter:
+            if row["Kernel_Name"].startswith(("bwd_kernel", "bwd2_kernel", "bwd2n_kernel")) and row["Counter_Name"] == counter:
                 vals.append(float(row["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None, len(vals)
 
@@ -29,6 +29,7 @@ path = os.path.join(ROOT, "profiles", "traffic.json")
 d = json.load(open(path)) if os.path.exists(path) else {}
 d[prec] = {"B": B, "T": T, "k": k, "bytes_per_launch": bytes_per_launch, "fetch_kib_raw": fetch,
            "write_kib": write, "launches": [nf, nw],
-           "note": "bwd_kernel; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, mean over launches"}
+           "note": "flow backward (bwd2_kernel at the AR shapes); FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, "
+                   "mean over the step's launches"}
 json.dump(d, open(path, "w"), indent=1)
 print(json.dumps(d[prec]))

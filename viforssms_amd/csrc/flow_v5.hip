@@ -2092,7 +2092,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
 // does, with the position contractions at K = 32 over the pair; the hidden activations I_0 .. I_3 stay in
 // registers as bf16 pairs (what the one-sample kernel read back from its images) and each is written into the
 // wave's image slot 0 only when its weight gradient is formed, next to D_l in slot 1, so two 32-row image
-// slots per wave suffice (the one-sample kernel kept four 16-row slots).  k <= 32, one window.
+// slots per wave suffice (the one-sample kernel kept four 16-row slots).  k <= 24, one window.
 // ---------------------------------------------------------------------------
 constexpr int NW3 = 4;
 constexpr int NT3 = 64 * NW3;
@@ -2123,6 +2123,8 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
   static_assert(KB == 1, "k <= 32");
   constexpr int s = S2 ? 2 : 1;
   constexpr int KP = 16 * JB;
+  constexpr int KR = JB == 1 ? 16 : 24;      // dcon rows (k <= KR)
+  constexpr int QWR = s * P + KR;            // dcon[j][p] at column s p + j: du[q] = sum_j row_j[q], no masks
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW3][2][2 * P * HP];  // slot 0: I_l, slot 1: D_l, then dA0
   __shared__ float dthl[NW3][S][DTH];
@@ -2131,10 +2133,11 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
   __shared__ float gsc[NW3][2][2][P];  // per sample: sigma, the even outputs' pass-through gradient (stride 2)
   __shared__ float uwin[NW3][2][64];
   __shared__ float gwin[NW3][2][s * P];
-  __shared__ float dscr[NW3][2][KP][P];  // dcon[j][p]
+  __shared__ float dscr[NW3][KR][QWR];  // one sample at a time
   load_shared<NH, KB, JB, NP, NT3>(sh, img, cst);
   for (int i = threadIdx.x; i < NW3 * S * DTH; i += NT3) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW3 * S * KP; i += NT3) (&carry[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW3 * KR * QWR; i += NT3) (&dscr[0][0][0])[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW3 + w);
@@ -2377,6 +2380,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
       fence();
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
+      f4 dcn_keep[2][JB];
       if constexpr (DU) {
         f4 dcn[2][JB];
 #pragma unroll
@@ -2396,12 +2400,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int jb = 0; jb < JB; ++jb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int j = 16 * jb + 4 * g + r;
-              if (j < a.k) dscr[w][cb][j][c] = dcn[cb][jb][r];
-            }
+          for (int jb = 0; jb < JB; ++jb) dcn_keep[cb][jb] = dcn[cb][jb];
       }
       fence();
       f4 dth4[4];
@@ -2430,22 +2429,31 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
       }
-      // ---- du over local positions q in [0, fin + k) of each sample: transposed conv + pass-through + carry
+      // ---- du over local positions q in [0, fin + k) of each sample in turn: its dcon into the padded rows,
+      //      then one lane per position sums the rows (reads first, then a pairwise sum)
       if constexpr (DU) {
-        fence();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           if (cb == 1 && !two) break;
+          fence();
+#pragma unroll
+          for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int j = 16 * jb + 4 * g + r;
+              if (j < KR && j < a.k) dscr[w][j][s * c + j] = dcn_keep[cb][jb][r];
+            }
           const int q = lane;
           if (q < fin + a.k) {
-            float v = 0.f;
-            for (int j = 0; j < a.k; ++j) {
-              const int t = q - j;
-              const int pp = S2 ? (t >> 1) : t;
-              const bool ok = t >= 0 && pp < nP && (!S2 || !(t & 1));
-              const float x = dscr[w][cb][j][pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp)];
-              v += ok ? x : 0.f;
-            }
+            const int qc = q < QWR ? q : QWR - 1;
+            float t[KR];
+#pragma unroll
+            for (int j = 0; j < KR; ++j) t[j] = dscr[w][j][qc];
+#pragma unroll
+            for (int w2 = 1; w2 < KR; w2 *= 2)
+#pragma unroll
+              for (int j = 0; j + w2 < KR; j += 2 * w2) t[j] += t[j + w2];
+            float v = t[0];
             const int oq2 = q - a.k;
             if (oq2 >= 0 && oq2 < fin) {
               if constexpr (S2) v += (oq2 & 1) ? gwin[w][cb][oq2] * gsc[w][cb][0][oq2 >> 1] : gsc[w][cb][1][oq2 >> 1];
@@ -2687,9 +2695,9 @@ static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
          d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S && !g.dcb;
 }
 
-// the three-hidden-layer two-sample backward: LV / FHN heads (k <= 32), one window
+// the three-hidden-layer two-sample backward: LV / FHN heads (k <= 24), one window
 static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 && d->k <= 32 && d->H <= kMaxH &&
+  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 && d->k <= 24 && d->H <= kMaxH &&
          d->n_win == 1 && g.S == S && !g.dcb;
 }
 
