@@ -240,6 +240,11 @@ int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N,
  * group: 4096 rows at the B = 65536 benchmark), exported for its parity test. */
 int vissm_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, void* stream);
 
+/* x[0..n) = hi + lo (bf16 planes, hi = bf16(x), lo = bf16(x - hi), round to nearest even): the operands of the
+ * split-bf16 GEMMs of LV's window-shared conv over its time-mixing features (no reference equivalent: the
+ * reference runs that conv in fp32, lotka_volterra_partial.py:78-82).  x 16-byte aligned, hi / lo 8-byte. */
+int vissm_split_bf16(const float* x, void* hi, void* lo, int64_t n, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;
  * lotka_volterra_partial.py:366-386; SV_dense.py:304-328) from device-resident

@@ -73,10 +73,13 @@ def test_lv_cfg_flow_shape_m1000(prec):
     _check(res, **TOL[prec])
 
 
-def test_lv_cfg_full_length():
-    """BASELINE configs[3] at its own length M = T = 5000 (kernel_ext 10062), B = 2, fp32."""
-    res = run_parity_case("lv", 2, 5000, 20, 3, 50, 5, 10, device=DEV, precision=0, condition=True)
-    _check(res, **TOL["fp32"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_lv_cfg_full_length(prec):
+    """BASELINE configs[3] at its own length M = T = 5000 (kernel_ext 10062), B = 3 (a two-sample pair and a
+    ghost-paired sample on the bf16 kernels), fp32 and the bench's bf16 (the two-sample three-layer backward,
+    the split-bf16 feature GEMMs)."""
+    res = run_parity_case("lv", 3, 5000, 20, 3, 50, 5, 10, device=DEV, precision=PREC[prec], condition=True)
+    _check(res, **TOL[prec])
 
 
 # tiles per t-chunk of the B = 65536 benchmark launch (SURVEY configs[1]) on each kernel family:

@@ -103,6 +103,7 @@ SIGNATURES = {
     "vissm_sqnorm": (_i32, [_c_void_p, _i64, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_reduce_rows": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
     "vissm_reduce_rows_bf16": (_i32, [_c_void_p, _c_void_p, _i64, _i64, _c_void_p]),
+    "vissm_split_bf16": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p]),
     "vissm_gather_windows": (_i32, [ctypes.POINTER(GatherDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_theta_num_params": (_i32, [_i32, _i32]),
     "vissm_theta_workspace_size": (_size_t, [ctypes.POINTER(ThetaDesc)]),

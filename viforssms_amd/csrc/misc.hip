@@ -210,6 +210,33 @@ int launch_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, 
   return VISSM_OK;
 }
 
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi), both round-to-nearest-even (the operands of the split-bf16
+// library GEMMs): one read of x, one write of each plane; four elements per thread, grid-stride
+__global__ __launch_bounds__(256) void split_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ hi,
+                                                         __bf16* __restrict__ lo, int64_t n) {
+  typedef __bf16 bf4v __attribute__((ext_vector_type(4)));
+  const int64_t n4 = n / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    bf4v h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      h[j] = static_cast<__bf16>(e[j]);
+      l[j] = static_cast<__bf16>(e[j] - static_cast<float>(h[j]));
+    }
+    reinterpret_cast<bf4v*>(hi)[i] = h;
+    reinterpret_cast<bf4v*>(lo)[i] = l;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - 4 * n4) {
+    const int64_t j = 4 * n4 + threadIdx.x;
+    const __bf16 h = static_cast<__bf16>(x[j]);
+    hi[j] = h;
+    lo[j] = static_cast<__bf16>(x[j] - static_cast<float>(h));
+  }
+}
+
 int launch_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, hipStream_t st) {
   if (R <= 0 || N <= 0) return VISSM_OK;
   // single pass: rows summed sequentially per column (deterministic)
@@ -394,6 +421,21 @@ int vissm_reduce_rows(const float* slab, float* out, int64_t R, int64_t N, void*
 int vissm_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, void* stream) {
   VISSM_CHECK_ARG(slab && out && R >= 0 && N >= 0, "reduce_rows_bf16: bad args");
   return launch_reduce_rows_bf16(slab, out, R, N, as_stream(stream));
+}
+
+int vissm_split_bf16(const float* x, void* hi, void* lo, int64_t n, void* stream) {
+  VISSM_CHECK_ARG(n >= 0, "split_bf16: bad size");
+  if (n == 0) return VISSM_OK;
+  VISSM_CHECK_ARG(x && hi && lo, "split_bf16: null pointer");
+  VISSM_CHECK_ARG((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(hi) & 7) == 0 &&
+                      (reinterpret_cast<uintptr_t>(lo) & 7) == 0,
+                  "split_bf16: x must be 16-byte and hi / lo 8-byte aligned");
+  const int64_t n4 = std::max<int64_t>(1, n / 4);
+  const unsigned blocks = static_cast<unsigned>(std::min<int64_t>((n4 + 255) / 256, 8192));
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, static_cast<__bf16*>(hi),
+                     static_cast<__bf16*>(lo), n);
+  VISSM_CHECK_LAUNCH("split_bf16");
+  return VISSM_OK;
 }
 
 size_t vissm_adamax_workspace_size(int64_t n) {

@@ -76,6 +76,36 @@ def base_logprob(eps: torch.Tensor, n_last: int) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------------------
+# split-bf16 operand planes
+# ---------------------------------------------------------------------------------------
+def _dense_layout(t: torch.Tensor) -> bool:
+    """t covers its storage span densely in some dimension order (a contiguous tensor or a permuted view of one)."""
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz > 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+def split_bf16(x: torch.Tensor):
+    """(hi, lo) bf16 planes with x = hi + lo to ~2^-16 relative (vissm_split_bf16, one pass over x), laid out with
+    x's strides: x may be a transposed view (LV's time-mixing features)."""
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise _lib.VissmError("split_bf16: fp32 GPU tensor expected (there is deliberately no CPU fallback)")
+    if not _dense_layout(x):
+        x = x.contiguous()
+    hi = torch.empty_strided(x.shape, x.stride(), dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_strided(x.shape, x.stride(), dtype=torch.bfloat16, device=x.device)
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.preserve_format)
+    check(_lib.load().vissm_split_bf16(ptr(x), ptr(hi), ptr(lo), x.numel(), _lib.stream_handle(x.device)),
+          "vissm_split_bf16")
+    return hi, lo
+
+
+# ---------------------------------------------------------------------------------------
 # window gather
 # ---------------------------------------------------------------------------------------
 def gather_windows(src: torch.Tensor, starts: torch.Tensor, out: torch.Tensor, n: int, length: int, C: int,
