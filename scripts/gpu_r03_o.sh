@@ -1,0 +1,7 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py tests/test_gpu_config_parity.py tests/test_gpu_golden.py tests/test_gpu_loop.py -k "sv or k50 or 50 or paper" > "$OUT/r03_o_tests.log" 2>&1
+rc=$?; grep -E "FAIL|passed|failed" "$OUT/r03_o_tests.log" | tail -8; [ $rc -le 1 ] || exit $rc
+for r in 1 2; do timeout -k 10 300 python -u bench.py --model sv --steps 4 --warmup 2 --cpu-baseline off --parity-line off --families off > "$OUT/r03_o_sv.json" 2>"$OUT/r03_o_sv.err" || { tail -5 "$OUT/r03_o_sv.err"; exit 4; }
+python -c "import json;d=json.load(open('$OUT/r03_o_sv.json'));r=d['roofline'];print('sv', round(d['ms_per_step'],2), round(r['avg_launch_ms'],2), {k:round(v['avg_launch_ms'],2) for k,v in r['variants'].items()}, round(r['fwd_kernel_avg_ms'],2), '%.3e' % d['value'])"; done

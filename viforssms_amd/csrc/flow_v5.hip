@@ -826,9 +826,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   __shared__ float gwin[NW][64];
   // dcon[j][p] stored at its output position q = s p + j of row j (other columns stay zero),
   // so du[q] = sum_{j<k} row_j[q] needs no masks
-  // (k > 32: the unpadded [j][p] layout with a masked sum keeps the block's LDS in bounds)
+  // (k > 32: the [j][p] layout, row stride P + 1, summed along the diagonal q = s p + j -- at most P terms per q
+  // -- keeps the block's LDS in bounds)
   constexpr bool PADDED = JB <= 2;
-  constexpr int QW = PADDED ? 2 * P + KP : P;
+  constexpr int QW = PADDED ? 2 * P + KP : P + 1;
   __shared__ float dscr[NW][KP][QW];
   __shared__ float zls[FZ ? NW : 1][FZ ? S : 1][P];  // FZ: per-sample, per-column log sigma sums over the tiles
   __shared__ float zcar[FZ ? NW : 1][FZ ? S : 1];     // FZ: x at the previous tile's last position
@@ -1271,12 +1272,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
               for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
             }
           } else {
-#pragma unroll 4
-            for (int j = 0; j < a.k; ++j) {
-              const int t = q - j;
-              const int pp = a.s == 1 ? t : (t >> 1);
-              const bool ok = t >= 0 && pp < nP && (a.s == 1 || !(t & 1));
-              const float x = dsc[j * P + (pp < 0 ? 0 : (pp > P - 1 ? P - 1 : pp))];
+            // the diagonal q = s p + j over the tile's P positions (columns p >= nP hold zeros: their gradients
+            // are zero); row stride P + 1 puts the 64 lanes' reads of one p in 64 distinct banks.  (Round 2 summed
+            // all k rows with a mask per term: SV's k = 50 made the du section 46 % of the launch.)
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+              const int j = q - a.s * p;
+              const bool ok = static_cast<unsigned>(j) < static_cast<unsigned>(a.k);
+              const float x = dsc[(ok ? j : 0) * QW + p];
               v += ok ? x : 0.f;
             }
           }
