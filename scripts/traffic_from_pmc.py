@@ -15,7 +15,9 @@ def per_launch(counter):
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{counter}", "**", "*counter_collection.csv"),
                        recursive=True):
         for row in csv.DictReader(open(f)):
-            if row["Kernel_Name"].startswith(("bwd_kernel", "bwd2_kernel", "bwd2n_kernel")) and row["Counter_Name"] == counter:
+            n = row["Kernel_Name"]
+            flow_bwd = n.startswith(("bwd_kernel", "bwd2_kernel", "bwd2n_kernel")) or ("flow5" in n and "bwd" in n)
+            if flow_bwd and row["Counter_Name"] == counter:
                 vals.append(float(row["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None, len(vals)
 
