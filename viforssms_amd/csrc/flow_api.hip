@@ -26,6 +26,15 @@ int flow5_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const 
 int flow5_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*, size_t, hipStream_t);
 
+// the same kernels built without the SLP vectorizer (flow_v5n.hip): the three-hidden-layer shapes
+bool flow5_supports_nh3(const VissmFlowDesc* d);
+size_t flow5_workspace_size_nh3(const VissmFlowDesc* d, int backward);
+int flow5_fwd_nh3(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*,
+                  const float*, float*, float*, void*, size_t, hipStream_t);
+int flow5_bwd_nh3(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*,
+                  const float*, const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*,
+                  size_t, hipStream_t);
+
 bool flow5_ar_fused_supports(const VissmFlowDesc* d);
 size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d);
 int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -56,6 +65,10 @@ static int validate(const VissmFlowDesc* d) {
 // cover the shape; anything else runs the exact-fp32 kernels (never less precise
 // than requested).
 static bool use_v5(const VissmFlowDesc* d) { return d->precision != VISSM_PREC_FP32 && flow5_supports(d); }
+// three hidden layers with k <= 24 (the two-sample backward's shapes: LV, FHN): the build without the SLP vectorizer
+// (flow_v5n.hip; LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5 ms per launch).  SV's k = 50 runs the one-sample
+// kernel, which measured slower that way (10.3 -> 10.8 ms).
+static bool use_nh3(const VissmFlowDesc* d) { return d->n_hidden == 3 && d->k <= 24; }
 
 }  // namespace vissm
 
@@ -65,7 +78,7 @@ extern "C" {
 
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
-  if (use_v5(d)) return flow5_workspace_size(d, backward);
+  if (use_v5(d)) return use_nh3(d) ? flow5_workspace_size_nh3(d, backward) : flow5_workspace_size(d, backward);
   return use_flow4(d) ? flow4_workspace_size(d, backward) : flow2_workspace_size(d, backward);
 }
 
@@ -80,7 +93,9 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (w->bn_g && w->bn_b), "flow_fwd: bn needs bn_g/bn_b");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
-  if (use_v5(d)) return flow5_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
+  if (use_v5(d))
+    return (use_nh3(d) ? flow5_fwd_nh3 : flow5_fwd)(d, w, u, C, win, theta_term, u_next, logsig, workspace,
+                                                          ws_bytes, st);
   if (use_flow4(d)) return flow4_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
   return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
 }
@@ -103,7 +118,8 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
-    return flow5_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
+    return (use_nh3(d) ? flow5_bwd_nh3 : flow5_bwd)(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC,
+                                                          dtheta_term, gr, workspace, ws_bytes, st);
   if (use_flow4(d))
     return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
   return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);

@@ -37,10 +37,17 @@
 // two samples per unit, see below.  Everything else runs on flow_v4 / flow_v2 (exact fp32).
 #include "common.hpp"
 
+// flow_v5n.hip compiles this file a second time, without the SLP vectorizer, under its own namespace and entry
+// point names: the three-hidden-layer shapes (LV / SV / FHN) dispatch there (flow_api.hip)
+#ifndef VISSM_FLOW5_NS
+#define VISSM_FLOW5_NS flow5
+#define VISSM_FLOW5_API(name) name
+#endif
+
 #include <cstdlib>
 
 namespace vissm {
-namespace flow5 {
+namespace VISSM_FLOW5_NS {
 
 constexpr int P = 16;
 constexpr int HP = 64;
@@ -2710,11 +2717,11 @@ static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
          d->k <= 16 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
 }
 
-}  // namespace flow5
+}  // namespace VISSM_FLOW5_NS
 
-using namespace flow5;
+using namespace VISSM_FLOW5_NS;
 
-bool flow5_supports(const VissmFlowDesc* d) {
+bool VISSM_FLOW5_API(flow5_supports)(const VissmFlowDesc* d) {
   // one hidden layer (AR): bf16 and bf16x3 (k <= 32: hi + lo images in LDS); three hidden layers
   // with or without BN (LV / SV / FHN heads): bf16
   if (d->H > kMaxH || d->k > 64) return false;
@@ -2724,7 +2731,7 @@ bool flow5_supports(const VissmFlowDesc* d) {
   return false;
 }
 
-size_t flow5_workspace_size(const VissmFlowDesc* d, int backward) {
+size_t VISSM_FLOW5_API(flow5_workspace_size)(const VissmFlowDesc* d, int backward) {
   Geom g = geom(d, backward != 0);
   return ws_layout(d, g, backward != 0, nullptr, nullptr);
 }
@@ -2790,7 +2797,7 @@ static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const 
                      d->bn, np_of(d), KB, JB, ws.img, ws.cst);
 }
 
-int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
               const float* theta_term, float* u_next, float* logsig, void* workspace, size_t ws_bytes,
               hipStream_t st) {
   Geom g = geom(d, false);
@@ -2822,7 +2829,7 @@ int flow5_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   return launch_reduce_rows(ws.ls_slab, logsig, g.n_chunks, d->B, st);
 }
 
-int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
               const float* theta_term, const float* du_next, const float* dlogsig, float* du, float* dC,
               float* dtheta_term, const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st) {
   Geom g = geom(d, true);
@@ -2887,7 +2894,7 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   const int nW = n_wgrad(d);
   rc = launch_reduce_rows_inplace(ws.dW_slab, ws.wred, g.n_items, nW, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
+  hipLaunchKernelGGL(VISSM_FLOW5_NS::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
                      d->H, d->n_hidden, d->bn);
   VISSM_CHECK_LAUNCH("flow5_scatter");
   return VISSM_OK;
@@ -2895,12 +2902,12 @@ int flow5_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
 
 
 // ---- the last AR(1) flow fused with its ELBO terms (vissm_flow_ar_elbo_fused) ----
-bool flow5_ar_fused_supports(const VissmFlowDesc* d) {
+bool VISSM_FLOW5_API(flow5_ar_fused_supports)(const VissmFlowDesc* d) {
   return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && d->n_hidden == 1 && !d->bn &&
          !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH && d->n_win >= 1;
 }
 
-size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d) {
+size_t VISSM_FLOW5_API(flow5_ar_fused_workspace_size)(const VissmFlowDesc* d) {
   Geom g = geom(d, true, P - 1);
   return ws_layout(d, g, true, nullptr, nullptr, true);
 }
@@ -2916,7 +2923,7 @@ size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d) {
     }                                                                                      \
   } while (0)
 
-int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
+int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
                    const float* theta_term, const float* theta, const float* obs, const float* obs_bin, float obs_std,
                    float scale, float* x, float* logsig, float* du, float* dC, float* dtheta_term,
                    const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st) {
@@ -2969,7 +2976,7 @@ int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   const int nW = n_wgrad(d);
   rc = launch_reduce_rows_inplace(ws.dW_slab, ws.wred, g.n_items, nW, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(flow5::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
+  hipLaunchKernelGGL(VISSM_FLOW5_NS::scatter_wgrad_kernel, dim3((nW + 255) / 256), dim3(256), 0, st, ws.wred, *w, *gr, d->k,
                      d->H, d->n_hidden, d->bn);
   VISSM_CHECK_LAUNCH("flow5_fused_scatter");
   return VISSM_OK;
