@@ -105,6 +105,12 @@ BF16_FAMILY_TOL = dict(elbo_tol=5e-3, grad_tol=2e-2, param_tol=2e-1)
     ("sv", 4, 24, 6, 2, 16, 5, 3),
     ("sv", 3, 52, 50, 5, 50, 5, 5),
     ("fhn", 3, 50, 20, 3, 50, 5, 10),
+    # the two-sample three-layer backward's k edges: 24 (padded dcon rows, stride 2), 33 and 64 (diagonal du sum,
+    # JB = 3, 4; odd B: a ghost-paired sample), 28 (between the two: the one-sample kernel)
+    ("lv", 5, 40, 24, 2, 32, 5, 3),
+    ("sv", 5, 60, 33, 2, 50, 5, 5),
+    ("sv", 4, 80, 64, 2, 50, 5, 5),
+    ("sv", 3, 40, 28, 2, 24, 5, 3),
 ])
 def test_family_parity_matrix_core(family, B, M, k, nf, H, nl, fw):
     _check(run_parity_case(family, B, M, k, nf, H, nl, fw, device=DEV, precision=1), **BF16_FAMILY_TOL)

@@ -65,10 +65,12 @@ static int validate(const VissmFlowDesc* d) {
 // cover the shape; anything else runs the exact-fp32 kernels (never less precise
 // than requested).
 static bool use_v5(const VissmFlowDesc* d) { return d->precision != VISSM_PREC_FP32 && flow5_supports(d); }
-// three hidden layers with k <= 24 (the two-sample backward's shapes: LV, FHN): the build without the SLP vectorizer
-// (flow_v5n.hip; LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5 ms per launch).  SV's k = 50 runs the one-sample
-// kernel, which measured slower that way (10.3 -> 10.8 ms).
-static bool use_nh3(const VissmFlowDesc* d) { return d->n_hidden == 3 && d->k <= 24; }
+// three hidden layers on one window with the two-sample backward's k (LV, FHN: k <= 24; SV: 32 < k <= 64, stride 1): the
+// build without the SLP vectorizer (flow_v5n.hip; LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5, SV 7.2 -> 6.7 ms
+// per launch).  The one-sample three-layer kernel (several windows) measured slower that way (SV: 10.3 -> 10.8 ms).
+static bool use_nh3(const VissmFlowDesc* d) {
+  return d->n_hidden == 3 && d->n_win == 1 && (d->k <= 24 || (d->k > 32 && d->k <= 64 && !d->stride2));
+}
 
 }  // namespace vissm
 

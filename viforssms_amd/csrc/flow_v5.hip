@@ -2102,7 +2102,8 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
 // does, with the position contractions at K = 32 over the pair; the hidden activations I_0 .. I_3 stay in
 // registers as bf16 pairs (what the one-sample kernel read back from its images) and each is written into the
 // wave's image slot 0 only when its weight gradient is formed, next to D_l in slot 1, so two 32-row image
-// slots per wave suffice (the one-sample kernel kept four 16-row slots).  k <= 24, one window.
+// slots per wave suffice (the one-sample kernel kept four 16-row slots).  k <= 24 (any stride) or 32 < k <= 64
+// (stride 1: SV), one window.
 // ---------------------------------------------------------------------------
 constexpr int NW3 = 4;
 constexpr int NT3 = 64 * NW3;
@@ -2111,6 +2112,9 @@ constexpr int NT3 = 64 * NW3;
 #endif
 #ifndef VISSM_BWD2N_MED3
 #define VISSM_BWD2N_MED3 1
+#endif
+#ifndef VISSM_BWD2N_K64
+#define VISSM_BWD2N_K64 1  // the two-sample kernel also for 32 < k <= 64 (SV's k = 50), stride 1
 #endif
 
 __device__ __forceinline__ void put_pairs(__bf16* img, const u2 (&v)[4], int g, int c) {
@@ -2130,18 +2134,22 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
                                                        float* __restrict__ dC_slab, float* __restrict__ dth_slab,
                                                        float* __restrict__ dW_slab, float* __restrict__ halo) {
   constexpr int NH = 3, KB = (JB + 1) / 2, NP = 1;
-  static_assert(KB == 1, "k <= 32");
+  static_assert(JB <= 2 || !S2, "k > 32: stride 1 only");
   constexpr int s = S2 ? 2 : 1;
   constexpr int KP = 16 * JB;
-  constexpr int KR = JB == 1 ? 16 : 24;      // dcon rows (k <= KR)
-  constexpr int QWR = s * P + KR;            // dcon[j][p] at column s p + j: du[q] = sum_j row_j[q], no masks
+  // dcon rows: k <= 24 (JB <= 2) at column s p + j of row j (padded: du[q] = sum_j row_j[q], no masks); k > 32 in
+  // [j][p] rows of stride P + 1 (no room for padded rows), summed along the diagonal q = p + j (at most P terms)
+  constexpr bool DIAG = JB > 2;
+  constexpr int KR = JB == 1 ? 16 : JB == 2 ? 24 : KP;
+  constexpr int QWR = DIAG ? P + 1 : s * P + KR;
+  constexpr int UWN = KB == 1 ? 64 : 128;    // u entries staged per sample (s P + k of them read)
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW3][2][2 * P * HP];  // slot 0: I_l, slot 1: D_l, then dA0
   __shared__ float dthl[NW3][S][DTH];
   __shared__ __attribute__((aligned(16))) float dths[NW3][4];
   __shared__ float carry[NW3][S][KP];
   __shared__ float gsc[NW3][2][2][P];  // per sample: sigma, the even outputs' pass-through gradient (stride 2)
-  __shared__ float uwin[NW3][2][64];
+  __shared__ float uwin[NW3][2][UWN];
   __shared__ float gwin[NW3][2][s * P];
   __shared__ float dscr[NW3][KR][QWR];  // one sample at a time
   load_shared<NH, KB, JB, NP, NT3>(sh, img, cst);
@@ -2189,10 +2197,12 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
       const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
       f4 X[2][4];
       {
-        float uv[2], gv[2] = {0.f, 0.f};
+        float uv[2][UWN / 64], gv[2] = {0.f, 0.f};
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          uv[cb] = lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane, a.L)] : 0.f;
+#pragma unroll
+          for (int i = 0; i < UWN / 64; ++i)
+            uv[cb][i] = lane + 64 * i < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane + 64 * i, a.L)] : 0.f;
           if (lane < s * P) {
             const int o = t0 + lane;
             gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.Lout + clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
@@ -2211,7 +2221,8 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          uwin[w][cb][lane] = uv[cb];
+#pragma unroll
+          for (int i = 0; i < UWN / 64; ++i) uwin[w][cb][lane + 64 * i] = uv[cb][i];
           if (lane < s * P) gwin[w][cb][lane] = gv[cb];
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
@@ -2223,12 +2234,15 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
       {
         f4 acc[2][4];
         fence();
-        const Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], s, 0, g, c), u_frag<NP>(uwin[w][1], s, 0, g, c)};
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-          const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
+        for (int kb = 0; kb < KB; ++kb) {
+          const Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], s, kb, g, c), u_frag<NP>(uwin[w][1], s, kb, g, c)};
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], X[cb][ob]);
+          for (int ob = 0; ob < 4; ++ob) {
+            const Fr8<NP> wf = wfrag(sh, 16 * NH + kb * 4 + ob, lane);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
+          }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
@@ -2412,6 +2426,8 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int jb = 0; jb < JB; ++jb) dcn_keep[cb][jb] = dcn[cb][jb];
       }
+      // dW_eps and d theta from dA0's position-contracted fragments (K = 32 over the pair)
+      auto dth_block = [&]() {
       fence();
       f4 dth4[4];
       {
@@ -2439,6 +2455,8 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
       }
+      };
+      auto du_block = [&]() {
       // ---- du over local positions q in [0, fin + k) of each sample in turn: its dcon into the padded rows,
       //      then one lane per position sums the rows (reads first, then a pairwise sum)
       if constexpr (DU) {
@@ -2451,19 +2469,34 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int j = 16 * jb + 4 * g + r;
-              if (j < KR && j < a.k) dscr[w][j][s * c + j] = dcn_keep[cb][jb][r];
+              if (DIAG) dscr[w][j][c] = dcn_keep[cb][jb][r];
+              else if (j < KR && j < a.k) dscr[w][j][s * c + j] = dcn_keep[cb][jb][r];
             }
-          const int q = lane;
+#pragma unroll
+          for (int base = 0; base < (DIAG ? 128 : 64); base += 64) {
+          const int q = base + lane;
           if (q < fin + a.k) {
-            const int qc = q < QWR ? q : QWR - 1;
-            float t[KR];
+            float v;
+            if constexpr (DIAG) {
+              v = 0.f;
 #pragma unroll
-            for (int j = 0; j < KR; ++j) t[j] = dscr[w][j][qc];
+              for (int p = 0; p < P; ++p) {
+                const int j = q - p;
+                const bool ok = static_cast<unsigned>(j) < static_cast<unsigned>(a.k);
+                const float x = dscr[w][ok ? j : 0][p];
+                v += ok ? x : 0.f;
+              }
+            } else {
+              const int qc = q < QWR ? q : QWR - 1;
+              float t[KR];
 #pragma unroll
-            for (int w2 = 1; w2 < KR; w2 *= 2)
+              for (int j = 0; j < KR; ++j) t[j] = dscr[w][j][qc];
 #pragma unroll
-              for (int j = 0; j + w2 < KR; j += 2 * w2) t[j] += t[j + w2];
-            float v = t[0];
+              for (int w2 = 1; w2 < KR; w2 *= 2)
+#pragma unroll
+                for (int j = 0; j + w2 < KR; j += 2 * w2) t[j] += t[j + w2];
+              v = t[0];
+            }
             const int oq2 = q - a.k;
             if (oq2 >= 0 && oq2 < fin) {
               if constexpr (S2) v += (oq2 & 1) ? gwin[w][cb][oq2] * gsc[w][cb][0][oq2 >> 1] : gsc[w][cb][1][oq2 >> 1];
@@ -2474,7 +2507,17 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
             if (q < fin) du[static_cast<size_t>(bv[cb]) * a.L + t0 + q] = v;
             else carry[w][blq][q - fin] = v;
           }
+          }
         }
+      }
+      };
+      // k > 32: the du section first, so the pair's dcon tiles are not live across the dW_eps / d theta products
+      if constexpr (DIAG) {
+        du_block();
+        dth_block();
+      } else {
+        dth_block();
+        du_block();
       }
     }
     if (c < nP) {
@@ -2705,10 +2748,13 @@ static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
          d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S && !g.dcb;
 }
 
-// the three-hidden-layer two-sample backward: LV / FHN heads (k <= 24), one window
+// the three-hidden-layer two-sample backward: LV / FHN heads (k <= 24: padded dcon rows), SV (32 < k <= 64, stride 1:
+// the diagonal du sum), one window
 static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 && d->k <= 24 && d->H <= kMaxH &&
-         d->n_win == 1 && g.S == S && !g.dcb;
+  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 &&
+         (d->k <= 24 || (VISSM_BWD2N_K64 && d->k > 32 && d->k <= 64 && !d->stride2)) && d->H <= kMaxH &&
+         d->n_win == 1 &&
+         g.S == S && !g.dcb;
 }
 
 // the two-sample forward covers the AR configurations' flow shape
@@ -2856,7 +2902,9 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
       else { if (du) BWD2N_LAUNCH(2, true, true); else BWD2N_LAUNCH(2, true, false); }
     } else {
       if (jb == 1) { if (du) BWD2N_LAUNCH(1, false, true); else BWD2N_LAUNCH(1, false, false); }
-      else { if (du) BWD2N_LAUNCH(2, false, true); else BWD2N_LAUNCH(2, false, false); }
+      else if (jb == 2) { if (du) BWD2N_LAUNCH(2, false, true); else BWD2N_LAUNCH(2, false, false); }
+      else if (jb == 3) { if (du) BWD2N_LAUNCH(3, false, true); else BWD2N_LAUNCH(3, false, false); }
+      else { if (du) BWD2N_LAUNCH(4, false, true); else BWD2N_LAUNCH(4, false, false); }
     }
 #undef BWD2N_LAUNCH
   } else if (bwd2_ok(d, g)) {
