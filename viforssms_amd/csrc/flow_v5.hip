@@ -1454,6 +1454,18 @@ __device__ __forceinline__ void fence2() {
 #ifndef VISSM_BWD2_PRIO
 #define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
 #endif
+#ifndef VISSM_BWD2_FZTILE
+#define VISSM_BWD2_FZTILE 1  // fused variant: the tile's observations (per position, not per sample) loaded once per
+                             // tile instead of with every pair's inputs
+#endif
+#ifndef VISSM_BWD2_FZLOG
+#define VISSM_BWD2_FZLOG 1  // fused variant: log sigma on v_log_f32 (sigma >= 1e-10 is a normal float: __logf's
+                            // denormal scaling is dead code)
+#endif
+#ifndef VISSM_BWD2_FZDIAG
+#define VISSM_BWD2_FZDIAG 0  // timing-only ablations of the fused variant's own work (results wrong when set): 1 no x
+                             // stores, 2 no log sigma sums, 4 no obs loads, 8 no AR(1) stencil (upstream gradient 0)
+#endif
 
 // the K = 32 fragment of a position contraction: sample A's transposed fragment then sample B's
 __device__ __forceinline__ bf8 cat8(bf4 a, bf4 b) {
@@ -1542,6 +1554,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
     f4 dCa[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
+    float fz_yt = 0.f, fz_bt = 0.f;  // FZ (VISSM_BWD2_FZTILE): the observation of x_t (row t - 1) at p = c
+    if constexpr (FZ && VISSM_BWD2_FZTILE && !(VISSM_BWD2_FZDIAG & 4)) {
+      const int wo = min(max(m0 + c - 1, 0), fz.M - 1);
+      fz_yt = fz.obs[wo];
+      fz_bt = fz.bin[wo];
+    }
     for (int bl = 0; bl < nb; bl += 2) {
       fence2<FZ>();
       const bool two = bl + 1 < nb;  // wave-uniform; else the second slot is a ghost
@@ -1549,7 +1567,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
       // ---- inputs: the two u windows (and upstream-gradient windows), the shared C rows + each theta row
       f4 X[2][4];
-      float fz_yp = 0.f, fz_bp = 0.f, fz_zc[2] = {0.f, 0.f};
+      float fz_yp = fz_yt, fz_bp = fz_bt, fz_zc[2] = {0.f, 0.f};
       {
         float uv[2], gv[2] = {0.f, 0.f};
 #pragma unroll
@@ -1561,7 +1579,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           }
         }
         if (!two) gv[1] = 0.f;
-        if constexpr (FZ) {
+        if constexpr (FZ && !VISSM_BWD2_FZTILE && !(VISSM_BWD2_FZDIAG & 4)) {
           const int wo = min(max(m0 + c - 1, 0), fz.M - 1);
           fz_yp = fz.obs[wo];
           fz_bp = fz.bin[wo];
@@ -1679,13 +1697,15 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           const float zt = fh * (xn - th1 * x - th0) * is;
           const float zp = ft * (x - th1 * xp - th0) * is;
           const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
-          gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
-          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __logf(sig[cb]) : 0.f;
+          gmu[cb] = (cb == 0 || two) && !(VISSM_BWD2_FZDIAG & 8) ? -fz.scale * de : 0.f;
+          const float lsg = (t0 + c >= a.Lout - a.n_logsig)
+                                ? (VISSM_BWD2_FZLOG ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : __logf(sig[cb]))
+                                : 0.f;
           if (g == 0) {
             gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the rest of the unit reads
             if (pv && (cb == 0 || two)) {
-              fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
-              zls[w][bl2][c] += lsg;
+              if constexpr (!(VISSM_BWD2_FZDIAG & 1)) fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
+              if constexpr (!(VISSM_BWD2_FZDIAG & 2)) zls[w][bl2][c] += lsg;
             }
           }
           if (lane == PO - 1 && (nP == PO || discard) && (cb == 0 || two)) zcar[w][bl2] = x;
