@@ -7,7 +7,7 @@ L2 error of every product: forward, input gradient, weight gradient)."""
 import pytest
 import torch
 
-from viforssms_amd.linalg import linear_x3
+from viforssms_amd.linalg import linear_bf16, linear_x3
 from viforssms_amd.ops import split_bf16
 
 pytestmark = pytest.mark.gpu
@@ -65,3 +65,22 @@ def test_linear_x3_products_against_float64(batched, transposed):
     assert _rel(x.grad, dx64) < 1e-5
     assert _rel(W.grad, dW64) < 1e-5
     assert torch.allclose(b.grad.double(), dy64.reshape(-1, N).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_linear_bf16_products_at_bf16_accuracy(transposed):
+    """The single-bf16 alternative (VISSM_FEATURE_GEMM=bf16): every product within the bf16 operand rounding
+    (~2^-9 relative per operand; 1e-2 relative L2 over the products' 1031-term sums), gradients in the layout of x."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    Lf, CF, N = 515, 1031, 200
+    x = torch.randn(CF, Lf, device=DEV, generator=g).t() if transposed else torch.randn(Lf, CF, device=DEV, generator=g)
+    x = x.detach().requires_grad_(True)
+    W = (torch.randn(CF, N, device=DEV, generator=g) * 0.03).requires_grad_(True)
+    dy = torch.randn(Lf, N, device=DEV, generator=g)
+    y = linear_bf16(x, W)
+    y.backward(dy)
+    x64, W64, dy64 = x.detach().double(), W.detach().double(), dy.double()
+    assert _rel(y, x64 @ W64) < 1e-2
+    assert _rel(x.grad, dy64 @ W64.t()) < 1e-2
+    assert _rel(W.grad, x64.t() @ dy64) < 1e-2
+    assert x.grad.stride() == x.stride()

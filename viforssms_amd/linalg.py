@@ -122,6 +122,39 @@ class _LinearX3(torch.autograd.Function):
         return dx, dW, db
 
 
+class _LinearB1(torch.autograd.Function):
+    """y = x W (+ b) with every product on single bf16 operands and fp32 accumulation / output (the flow kernels'
+    own precision class; A/B alternative to _LinearX3)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        xb, Wb = x.to(torch.bfloat16), W.to(torch.bfloat16)
+        ctx.save_for_backward(xb, Wb)
+        ctx.has_b = b is not None
+        y = _mm(xb, Wb)
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, Wb = ctx.saved_tensors
+        dyb = dy.to(torch.bfloat16)
+        dx = dW = None
+        if ctx.needs_input_grad[0]:
+            dx = _t(_mm(Wb, _t(dyb))) if (xb.stride(-2) == 1 and xb.shape[-2] > 1) else _mm(dyb, _t(Wb))
+        if ctx.needs_input_grad[1]:
+            g = _mm(_t(xb), dyb)
+            dW = g.sum(0) if g.dim() == 3 else g
+        db = dy.reshape(-1, dy.shape[-1]).sum(0) if ctx.has_b else None
+        return dx, dW, db
+
+
+def linear_bf16(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """linear() with single-bf16 matrix-core products; CPU tensors (host tests) take linear()."""
+    if not x.is_cuda:
+        return linear(x, W, b)
+    return _LinearB1.apply(x, W, b)
+
+
 def linear_x3(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """linear() with split-bf16 (bf16x3) matrix-core products; CPU tensors (host tests) take linear()."""
     if not x.is_cuda:

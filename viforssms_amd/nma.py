@@ -28,7 +28,7 @@ from .ops import (FlowShape, ma_flow, normal_base, normal_base_dev, base_logprob
                   AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
-from .linalg import linear, linear_x3, tn_split_k
+from .linalg import linear, linear_bf16, linear_x3, tn_split_k
 
 LOG_2PI = math.log(2 * math.pi)
 
@@ -179,7 +179,7 @@ class IAF:
             h = h.transpose(1, 2)
         return h
 
-    def conv_shared(self, F: torch.Tensor, Lh: int, s: int, split_bf16: bool = False) -> torch.Tensor:
+    def conv_shared(self, F: torch.Tensor, Lh: int, s: int, gemm: Optional[str] = None) -> torch.Tensor:
         """C[w, m, :] = conv_b + sum_j F[w, s m + j, :] @ conv_w[j, 1:, :]  (valid conv over the features).
 
         One GEMM against all k taps at once, G = F @ [W_0 | ... | W_{k-1}]  ([.., Lf, k H]), then the
@@ -189,9 +189,10 @@ class IAF:
         k, H = self.spec.k, self.spec.H
         nw, Lf, CF = F.shape
         Wcat = W[:, 1:, :].permute(1, 0, 2).reshape(CF, k * H)
-        # (split_bf16: the three-product bf16 form, fp32-class, for the bf16 training precisions -- LV's
-        #  [10061 x 10061] feature matrix makes this the step's largest GEMM)
-        G = (linear_x3 if split_bf16 else linear)(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV)
+        # (gemm "x3": the three-product split-bf16 form, fp32-class, for the bf16 training precisions -- LV's
+        #  [10061 x 10061] feature matrix makes this the step's largest GEMM; "bf16": single bf16 products)
+        lin = {"x3": linear_x3, "bf16": linear_bf16}.get(gemm, linear)
+        G = lin(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV)
         return (_DiagSum.apply(G.contiguous(), Lh, s) + self._p("conv/bias")).contiguous()
 
     def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
@@ -387,7 +388,7 @@ class Engine:
             ts = batch.ts if md.family == "lv" else batch.ts[:, i * md.k:, :]
             F = fl.features(ts)
             Lh = (L - md.k) // s
-            C = fl.conv_shared(F, Lh, s, split_bf16=self.split_feature_gemm())
+            C = fl.conv_shared(F, Lh, s, gemm=self.feature_gemm())
             tt = fl.theta_term(theta)
             pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
@@ -419,10 +420,14 @@ class Engine:
                          swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
                          chunk_tiles=self.chunk_tiles)
 
-    def split_feature_gemm(self) -> bool:
-        """The window-shared conv over features as split-bf16 products: at the bf16 training precisions and
-        only where that GEMM is large (LV: the time-mixing features have kernel_ext - 1 channels)."""
-        return self.precision != _lib.VISSM_PREC_FP32 and self.mdef.family == "lv"
+    def feature_gemm(self) -> Optional[str]:
+        """How the window-shared conv over features runs: split-bf16 products ("x3") at the bf16 training
+        precisions where that GEMM is large (LV: the time-mixing features have kernel_ext - 1 channels), fp32
+        otherwise (None).  VISSM_FEATURE_GEMM=bf16 | x3 | fp32 overrides it (A/B)."""
+        env = os.environ.get("VISSM_FEATURE_GEMM")
+        if env:
+            return None if env == "fp32" else env
+        return "x3" if (self.precision != _lib.VISSM_PREC_FP32 and self.mdef.family == "lv") else None
 
     def flow_precisions(self):
         """(forward, backward) flow-kernel precisions of the engine's mode (host modes _lib.HOST_MODES:
