@@ -108,6 +108,16 @@ typedef struct {
   const float* bn_b;    /* [n_hidden][H] or NULL */
   const float* w_head;  /* [H][2]  (col 0 = mu, col 1 = sigma pre-softplus) */
   const float* b_head;  /* [2] */
+  /* Optional factorization of the theta branch (AR.py:63-68: three linear dense layers, so
+   * theta_term = theta_x w_theta + b_theta exactly).  theta_rank = 0 (or NULL pointers): unused.
+   * With 1 <= theta_rank <= 5 the bf16 AR kernels (one hidden layer, k <= 16, one window) form the
+   * theta term inside their layer-0 matrix product (split-bf16 theta and w_theta in its unused K
+   * rows) and add b_theta to C, instead of reading a [H] theta_term row per sample and unit; every
+   * other kernel reads theta_term.  theta_term must still be passed and equal the product. */
+  const float* theta_x; /* [B][theta_rank] per-sample theta (the q(theta) draw) */
+  const float* w_theta; /* [theta_rank][H] collapsed weight W0 W1 W2 */
+  const float* b_theta; /* [H] collapsed bias */
+  int32_t theta_rank;
 } VissmFlowParams;
 
 typedef struct {        /* outputs of the backward: written, not accumulated */

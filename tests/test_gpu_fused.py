@@ -83,3 +83,32 @@ def test_fused_equals_unfused(prec):
     tol = 1e-5 if prec == 2 else 2e-3
     assert float(((outs[0] - outs[1]).abs() / outs[1].abs()).max()) < tol
     assert float((grads[0] - grads[1]).norm() / grads[1].norm()) < (1e-4 if prec == 2 else 2e-2)
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+@pytest.mark.parametrize("chunk_tiles", [0, 167])
+def test_theta_fold_equals_theta_term(fuse, chunk_tiles, monkeypatch):
+    """The theta fold (VissmFlowParams.theta_rank: the two-sample AR kernels form theta_term = theta w_theta +
+    b_theta inside their layer-0 product from split-bf16 theta / w_theta, AR.py:63-72) against the same kernels
+    reading the fp32 theta_term rows: same model and draw, bf16, an odd sample count (a ghost partner in the last
+    pair), the automatic and the benchmark's chunk geometry, fused and unfused last flow.  The fold's products
+    carry ~2^-16 relative error, far inside the bf16 activations' rounding, so ELBO and gradient agree to the
+    run-to-run scale of that rounding."""
+    B, M, k = 33, 5000 if chunk_tiles else 500, 8
+    model = build_model("ar", B, M, k, 3, 50, 3, 10, DEV, precision=1, impute=5, condition=True)
+    model.engine.fuse_last = fuse
+    model.engine.chunk_tiles = chunk_tiles
+    batch = model.engine.make_batch(np.zeros(B, dtype=np.int64))
+    g = torch.Generator().manual_seed(11)
+    eps = torch.randn(B, model.mdef.kernel_ext, generator=g).to(DEV)
+    x0 = (torch.randn(B, 3, generator=g) * 0.5 + 1.5).to(DEV)
+    outs, grads = [], []
+    for fold in ("1", "0"):
+        monkeypatch.setenv("VISSM_THETA_FOLD", fold)
+        o = model.elbo_step(batch, 0, eps=eps, x0_theta=x0, apply=False)
+        torch.cuda.synchronize()
+        outs.append(o["elbo"].double().cpu())
+        grads.append(model.store.grad.double().cpu().clone())
+    assert torch.isfinite(outs[0]).all() and torch.isfinite(grads[0]).all()
+    assert float(((outs[0] - outs[1]).abs() / outs[1].abs()).max()) < 2e-4
+    assert float((grads[0] - grads[1]).norm() / grads[1].norm()) < 1e-2

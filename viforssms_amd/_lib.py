@@ -44,7 +44,8 @@ class FlowDesc(ctypes.Structure):
 
 
 class FlowParams(ctypes.Structure):
-    _fields_ = [(n, _c_void_p) for n in ("w_eps", "w_hid", "b_hid", "bn_g", "bn_b", "w_head", "b_head")]
+    _fields_ = ([(n, _c_void_p) for n in ("w_eps", "w_hid", "b_hid", "bn_g", "bn_b", "w_head", "b_head",
+                                          "theta_x", "w_theta", "b_theta")] + [("theta_rank", _i32)])
 
 
 class FlowGrads(ctypes.Structure):

@@ -305,8 +305,21 @@ __device__ __forceinline__ float bias_head(const VissmFlowParams& w, int H, int 
   return bb;
 }
 
+// theta fold (VissmFlowParams.theta_rank = R > 0, k <= 16): K rows 16 + kk of the layer-0 product carry the theta
+// term, theta_term[h] = sum_i w_theta[i][h] theta[i], as w_hi theta_hi + w_hi theta_lo + w_lo theta_hi:
+// kk < R: (w_hi[kk], theta_hi[kk]); R <= kk < 2R: (w_hi[kk - R], theta_lo[kk - R]); 2R <= kk < 3R: (w_lo, theta_hi)
+constexpr int kFoldRow = 16;
+__host__ __device__ __forceinline__ int fold_index(int kk, int R, int* which) {
+  if (kk < R) { *which = 0; return kk; }
+  if (kk < 2 * R) { *which = 1; return kk - R; }
+  if (kk < 3 * R) { *which = 2; return kk - 2 * R; }
+  *which = -1;
+  return -1;
+}
+__device__ __forceinline__ float bf16_hi(float x) { return static_cast<float>(static_cast<__bf16>(x)); }
+
 __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int NP, int KB, int JB,
-                            bf8* __restrict__ img, float* __restrict__ cst) {
+                            bf8* __restrict__ img, float* __restrict__ cst, int fold) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   const int NPL = NP >= 2 ? 2 : 1;
   float v[8];
@@ -326,6 +339,14 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
       const int kb = r >> 2, ob = r & 3;
       const int jt = 32 * kb + 8 * g + j, h = swz(16 * ob + c);
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
+      else if (fold && kb == 0 && jt >= kFoldRow && h < H) {  // the theta term's rows (theta fold)
+        int which;
+        const int i = fold_index(jt - kFoldRow, w.theta_rank, &which);
+        if (i >= 0) {
+          const float wv = w.w_theta[i * H + h] * kLog2e, hi = bf16_hi(wv);
+          x = which == 2 ? bf16_hi(wv - hi) : hi;
+        }
+      }
     } else if ((r -= 4 * KB) < 2 * JB) {  // WC
       const int jb = r >> 1, ks = r & 1;
       const int jt = 16 * jb + c, h = swz(hperm(ks, g, j));
@@ -369,13 +390,36 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
   }
 }
 
-// zero-padded 64-wide copies of C [n_win][Lh][H] and of the theta term [B][H], log2(e)-scaled
-__global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t rows, int H) {
+// zero-padded 64-wide copies of C [n_win][Lh][H] (+ the theta fold's bias) and of the theta term [B][H],
+// log2(e)-scaled
+__global__ void pad_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t rows, int H,
+                           const float* __restrict__ bias) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= rows * HP) return;
   const int64_t r = i / HP;
   const int h = swz(static_cast<int>(i % HP));
-  dst[i] = h < H ? src[r * H + h] * kLog2e : 0.f;
+  dst[i] = h < H ? (bias ? src[r * H + h] + bias[h] : src[r * H + h]) * kLog2e : 0.f;
+}
+
+// theta fold: per sample the B-operand rows 16..31 of the layer-0 product (lane groups 2, 3), as bf16:
+// tf[b][gg] = 8 values, kk = 8 gg + j (fold_index order)
+__global__ void theta_frag_kernel(const float* __restrict__ theta, int B, int R, u4* __restrict__ tf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * B) return;
+  const int b = i >> 1, gg = i & 1;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int which;
+    const int t = fold_index(8 * gg + j, R, &which);
+    float x = 0.f;
+    if (t >= 0) {
+      const float th = theta[static_cast<size_t>(b) * R + t], hi = bf16_hi(th);
+      x = which == 1 ? bf16_hi(th - hi) : hi;
+    }
+    v[j] = x;
+  }
+  tf[i] = u4{cvt2(v[0], v[1]), cvt2(v[2], v[3]), cvt2(v[4], v[5]), cvt2(v[6], v[7])};
 }
 
 template <int NH, int KB, int JB, int NP>
@@ -1478,14 +1522,14 @@ __device__ __forceinline__ bf8 tr_frag2(const __bf16* img, int hb, int g, int c)
   return cat8(tr_read(img, hb, g, c), tr_read(img + P * HP, hb, g, c));
 }
 
-template <bool FZ, bool DU>
+template <bool FZ, bool DU, bool TF>
 __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                       const float* __restrict__ tht, const float* __restrict__ gout,
                                                       const float* __restrict__ dls, const bf8* __restrict__ img,
                                                       const float* __restrict__ cst, float* __restrict__ du,
                                                       float* __restrict__ dC_slab, float* __restrict__ dth_slab,
                                                       float* __restrict__ dW_slab, float* __restrict__ halo,
-                                                      FzArgs fz = FzArgs{}) {
+                                                      const u4* __restrict__ thf, FzArgs fz = FzArgs{}) {
   constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
   constexpr int PO = FZ ? P - 1 : P;
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
@@ -1570,6 +1614,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
       // ---- inputs: the two u windows (and upstream-gradient windows), the shared C rows + each theta row
       f4 X[2][4];
+      bf8 tfr[2];
       float fz_yp = fz_yt, fz_bp = fz_bt, fz_zc[2] = {0.f, 0.f};
       {
         float uv[2], gv[2] = {0.f, 0.f};
@@ -1589,11 +1634,18 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         }
         const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nZ)) * HP) + g;
         f4 cr[4], tr[2][4];
+        if constexpr (TF) {  // the theta fold: the pair's theta rows of the layer-0 B operand (lane groups 2, 3)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) tfr[cb] = __builtin_bit_cast(bf8, thf[2 * static_cast<size_t>(bv[cb]) + (g & 1)]);
+        }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           cr[rb] = crow[4 * rb];
+          if constexpr (!TF) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+            for (int cb = 0; cb < 2; ++cb)
+              tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1601,7 +1653,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           uwin[w][cb][lane] = uv[cb];
           if (lane < P) gwin[w][cb][lane] = gv[cb];
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
+          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = TF ? cr[rb] : cr[rb] + tr[cb][rb];
         }
         if constexpr (FZ) {
           fz_zc[0] = zcar[w][blv[0]];
@@ -1615,6 +1667,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         f4 acc[2][4];
         fence2<FZ>();
         Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c), u_frag<NP>(uwin[w][1], 1, 0, g, c)};
+        if constexpr (TF) {
+          if (g >= 2) {
+            uf[0].h = tfr[0];
+            uf[1].h = tfr[1];
+          }
+        }
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
           const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
@@ -1979,19 +2037,27 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #ifndef VISSM_FWD2
 #define VISSM_FWD2 1
 #endif
+#ifndef VISSM_THETA_FOLD
+#define VISSM_THETA_FOLD 1  // the two-sample AR kernels form the theta term in the layer-0 product (fold_ok)
+#endif
 #ifndef VISSM_FWD2_REGW
 #define VISSM_FWD2_REGW 1
 #endif
 #ifndef VISSM_FWD2_OCC
 #define VISSM_FWD2_OCC 2
 #endif
+// TF: the theta fold (VissmFlowParams.theta_rank): the theta term rides in the layer-0 product's K rows 16..31
+// (lane groups 2, 3 of the B operand: the sample's fragment thf[b][g - 2], loaded once per pair) instead of a
+// [64] theta_term row per sample and tile added to the C rows
+template <bool TF>
 __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
                                                                   const bf8* __restrict__ img,
                                                                   const float* __restrict__ cst,
                                                                   float* __restrict__ u_next,
-                                                                  float* __restrict__ ls_slab) {
+                                                                  float* __restrict__ ls_slab,
+                                                                  const u4* __restrict__ thf) {
   constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][2][64];
@@ -2029,6 +2095,11 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
     const bool two = bl + 1 < nb;
     const int bv[2] = {b_lo + bl, b_lo + (two ? bl + 1 : bl)};
     float ls[2] = {0.f, 0.f};
+    bf8 tfr[2];  // TF: the pair's theta rows of the B operand (lane groups 2, 3)
+    if constexpr (TF) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) tfr[cb] = __builtin_bit_cast(bf8, thf[2 * static_cast<size_t>(bv[cb]) + (g & 1)]);
+    }
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
       const int nP = min(P, m_hi - m0), t0 = m0;
       f4 X[2][4];
@@ -2041,20 +2112,29 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           cr[rb] = crow[4 * rb];
+          if constexpr (!TF) {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+            for (int cb = 0; cb < 2; ++cb)
+              tr[cb][rb] = (reinterpret_cast<const f4*>(tht + static_cast<size_t>(bv[cb]) * HP) + g)[4 * rb];
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           uwin[w][cb][lane] = uv[cb];
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = cr[rb] + tr[cb][rb];
+          for (int rb = 0; rb < 4; ++rb) X[cb][rb] = TF ? cr[rb] : cr[rb] + tr[cb][rb];
         }
       }
       f4 acc[2][4];
       {
-        const bf8 uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c).h, u_frag<NP>(uwin[w][1], 1, 0, g, c).h};
+        bf8 uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c).h, u_frag<NP>(uwin[w][1], 1, 0, g, c).h};
+        if constexpr (TF) {
+          if (g >= 2) {
+            uf[0] = tfr[0];
+            uf[1] = tfr[1];
+          }
+        }
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
           const bf8 wf = W(16 * NH + ob, 8 * NH + ob);
@@ -2665,6 +2745,7 @@ struct Ws {
   bf8* img;
   float* cst;
   float *Cp, *thp;
+  u4* thf;                                               // theta fold: [B][2] B-operand rows
   float* ls_slab;                                        // fwd
   float *dC_slab, *dth_slab, *dW_slab, *halo, *wred;     // bwd
   float* zsl;                                            // fused AR(1) ELBO: per-chunk per-sample sums
@@ -2680,6 +2761,7 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   t.cst = reinterpret_cast<float*>(take(((d->n_hidden + 2) * HP + 4) * sizeof(float)));
   t.Cp = reinterpret_cast<float*>(take(static_cast<size_t>(d->n_win) * g.Lh * HP * 4));
   t.thp = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * HP * 4));
+  t.thf = reinterpret_cast<u4*>(take(static_cast<size_t>(d->B) * 2 * sizeof(u4)));
   if (!backward) {
     t.ls_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * 4));
   } else {
@@ -2851,19 +2933,31 @@ size_t VISSM_FLOW5_API(flow5_workspace_size)(const VissmFlowDesc* d, int backwar
     }                                                                                              \
   } while (0)
 
-static void launch_pad(const VissmFlowDesc* d, const Geom& g, const float* C, const float* tht, const Ws& ws,
-                       hipStream_t st) {
-  const int64_t nC = static_cast<int64_t>(d->n_win) * g.Lh, nT = d->B;
-  hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nC * HP + 255) / 256)), dim3(256), 0, st, C, ws.Cp, nC,
-                     d->H);
-  hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nT * HP + 255) / 256)), dim3(256), 0, st, tht, ws.thp, nT,
-                     d->H);
+// the caller supplied the theta branch's factors (VissmFlowParams.theta_rank) and the shape leaves K rows 16..31 of
+// the layer-0 product free
+static bool fold_ok(const VissmFlowDesc* d, const VissmFlowParams* w) {
+  return VISSM_THETA_FOLD && w->theta_rank >= 1 && w->theta_rank <= 5 && w->theta_x && w->w_theta && w->b_theta &&
+         d->k <= kFoldRow;
 }
 
-static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, hipStream_t st) {
+// padded C (+ b_theta when folding) and either the padded theta term or the theta fold's B-operand rows
+static void launch_pad(const VissmFlowDesc* d, const VissmFlowParams* w, const Geom& g, const float* C,
+                       const float* tht, const Ws& ws, bool fold, hipStream_t st) {
+  const int64_t nC = static_cast<int64_t>(d->n_win) * g.Lh, nT = d->B;
+  hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nC * HP + 255) / 256)), dim3(256), 0, st, C, ws.Cp, nC,
+                     d->H, fold ? w->b_theta : static_cast<const float*>(nullptr));
+  if (fold)
+    hipLaunchKernelGGL(theta_frag_kernel, dim3(static_cast<unsigned>((2 * nT + 255) / 256)), dim3(256), 0, st,
+                       w->theta_x, d->B, w->theta_rank, ws.thf);
+  else
+    hipLaunchKernelGGL(pad_kernel, dim3(static_cast<unsigned>((nT * HP + 255) / 256)), dim3(256), 0, st, tht, ws.thp,
+                       nT, d->H, static_cast<const float*>(nullptr));
+}
+
+static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, bool fold, hipStream_t st) {
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
   hipLaunchKernelGGL(prep_kernel, dim3(n_frags(d->n_hidden, KB, JB)), dim3(64), 0, st, *w, d->H, d->k, d->n_hidden,
-                     d->bn, np_of(d), KB, JB, ws.img, ws.cst);
+                     d->bn, np_of(d), KB, JB, ws.img, ws.cst, fold ? 1 : 0);
 }
 
 int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -2873,15 +2967,21 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   VISSM_CHECK_ARG(workspace && ws_bytes >= ws_layout(d, g, false, nullptr, nullptr), "flow_fwd: workspace too small");
   Ws ws;
   ws_layout(d, g, false, reinterpret_cast<char*>(workspace), &ws);
-  launch_prep(d, w, ws, st);
-  launch_pad(d, g, C, theta_term, ws, st);
+  const bool f2 = fwd2_ok(d, g), fold = f2 && fold_ok(d, w);
+  launch_prep(d, w, ws, fold, st);
+  launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
-  if (fwd2_ok(d, g)) {
-    hipLaunchKernelGGL(fwd2_kernel, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, ws.ls_slab);
+  if (f2) {
+    if (fold)
+      hipLaunchKernelGGL(fwd2_kernel<true>, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next,
+                         ws.ls_slab, ws.thf);
+    else
+      hipLaunchKernelGGL(fwd2_kernel<false>, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next,
+                         ws.ls_slab, ws.thf);
   } else if (np_of(d) == 2) {
     if (jb_of(d->k) == 1)
       hipLaunchKernelGGL((fwd_kernel<1, 1, 1, 2>), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst, u_next,
@@ -2905,8 +3005,9 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   VISSM_CHECK_ARG(workspace && ws_bytes >= ws_layout(d, g, true, nullptr, nullptr), "flow_bwd: workspace too small");
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws);
-  launch_prep(d, w, ws, st);
-  launch_pad(d, g, C, theta_term, ws, st);
+  const bool b2 = !bwd2n_ok(d, g) && bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
+  launch_prep(d, w, ws, fold, st);
+  launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
@@ -2930,14 +3031,14 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
       else { if (du) BWD2N_LAUNCH(4, false, true); else BWD2N_LAUNCH(4, false, false); }
     }
 #undef BWD2N_LAUNCH
-  } else if (bwd2_ok(d, g)) {
+  } else if (b2) {
     const dim3 grid2((g.n_items + NW2 - 1) / NW2);
-    if (du)
-      hipLaunchKernelGGL((bwd2_kernel<false, true>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig,
-                         ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, FzArgs{});
-    else
-      hipLaunchKernelGGL((bwd2_kernel<false, false>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig,
-                         ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, FzArgs{});
+#define BWD2_LAUNCH(DU_, TF_)                                                                                     \
+  hipLaunchKernelGGL((bwd2_kernel<false, DU_, TF_>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig, \
+                     ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, FzArgs{})
+    if (du) { if (fold) BWD2_LAUNCH(true, true); else BWD2_LAUNCH(true, false); }
+    else { if (fold) BWD2_LAUNCH(false, true); else BWD2_LAUNCH(false, false); }
+#undef BWD2_LAUNCH
   } else if (du)
     FLOW5_DISPATCH_T(bwd_kernel, false COMMA true, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
                      ws.Cp, wn, ws.thp, du_next, dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab,
@@ -3003,8 +3104,9 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
                   "flow_ar_elbo_fused: workspace too small");
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
-  launch_prep(d, w, ws, st);
-  launch_pad(d, g, C, theta_term, ws, st);
+  const bool b2 = bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
+  launch_prep(d, w, ws, fold, st);
+  launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_fused_prep");
   KArgs a = make_args(d, g);
   FzArgs fz;
@@ -3019,11 +3121,14 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   const int32_t* wn = d->n_win > 1 ? win : nullptr;
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(VISSM_PROF_FLOW_FUSED, st);
-  if (bwd2_ok(d, g))
-    hipLaunchKernelGGL((bwd2_kernel<true, true>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u, ws.Cp,
-                       ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst,
-                       du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);
-  else
+  if (b2) {
+#define BWD2F_LAUNCH(TF_)                                                                                            \
+  hipLaunchKernelGGL((bwd2_kernel<true, true, TF_>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u, ws.Cp, \
+                     ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst,    \
+                     du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, fz)
+    if (fold) BWD2F_LAUNCH(true); else BWD2F_LAUNCH(false);
+#undef BWD2F_LAUNCH
+  } else
     FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,
                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst, du,
                       ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, fz);

@@ -195,6 +195,18 @@ class IAF:
         G = lin(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV)
         return (_DiagSum.apply(G.contiguous(), Lh, s) + self._p("conv/bias")).contiguous()
 
+    def theta_factors(self, theta: torch.Tensor):
+        """(theta, w_theta, b_theta) with theta_term = theta w_theta + b_theta: the collapsed weights _ThetaBranch
+        forms (the same fp32 products), passed to the flow kernels as constants (VissmFlowParams.theta_rank) so
+        the two-sample AR kernels form the theta term inside their layer-0 product; the gradient still flows
+        through theta_term."""
+        p = self._p
+        with torch.no_grad():
+            W1, W2 = p("theta1/kernel"), p("theta2/kernel")
+            W12 = W1 @ W2
+            return (theta.detach().contiguous(), (p("theta0/kernel") @ W12).contiguous(),
+                    (p("theta0/bias") @ W12 + p("theta1/bias") @ W2 + p("theta2/bias")).contiguous())
+
     def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
         p = self._p
         return _ThetaBranch.apply(theta, p("theta0/kernel"), p("theta0/bias"), p("theta1/kernel"),
@@ -218,7 +230,7 @@ class IAF:
             bn_g = bn_b = None
         return w_eps, w_hid, b_hid, bn_g, bn_b, self._p("head/kernel"), self._p("head/bias")
 
-    def flow(self, shape: FlowShape, win, u, C, theta_term):
+    def flow(self, shape: FlowShape, win, u, C, theta_term, tf=None):
         s = self.spec
         w_eps = self._p("conv/kernel")[:, 0, :].contiguous()
         if s.n_hidden > 0:
@@ -232,7 +244,7 @@ class IAF:
         else:
             bn_g = bn_b = None
         return ma_flow(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b,
-                       self._p("head/kernel"), self._p("head/bias"))
+                       self._p("head/kernel"), self._p("head/bias"), tf)
 
 
 # ---------------------------------------------------------------------------------------
@@ -395,7 +407,7 @@ class Engine:
                               stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
                               n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
                               chunk_tiles=self.chunk_tiles)
-            u, ls = fl.flow(shape, batch.win, u, C, tt)
+            u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta))
             lq = lq - ls
             L -= md.k
         z = u
@@ -419,6 +431,15 @@ class Engine:
         return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
                          swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
                          chunk_tiles=self.chunk_tiles)
+
+    def theta_fold(self, fl: IAF, theta: torch.Tensor):
+        """The theta branch's factors for the flow kernels (IAF.theta_factors) at the bf16 products of the AR
+        family, whose two-sample kernels fold them into the layer-0 product; None elsewhere (the kernels read
+        theta_term).  VISSM_THETA_FOLD=0 turns it off (A/B)."""
+        if (self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or theta.shape[1] > 5
+                or os.environ.get("VISSM_THETA_FOLD", "1") == "0"):
+            return None
+        return fl.theta_factors(theta)
 
     def feature_gemm(self) -> Optional[str]:
         """How the window-shared conv over features runs: split-bf16 products ("x3") at the bf16 training
@@ -464,7 +485,7 @@ class Engine:
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
                               swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
                               chunk_tiles=self.chunk_tiles)
-            u, ls = fl.flow(shape, batch.win, u, C, tt)
+            u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta))
             lq = lq - ls
             L -= md.k
         fl = self.flows[-1]
@@ -479,7 +500,7 @@ class Engine:
         x, logsig, du, dC, dtt, gw = ar_last_flow_fused(
             shape, batch.win, u.detach().contiguous(), C.detach(), tt.detach(), theta.detach().contiguous(), f.obs,
             f.obs_bin, md.obs_std, scale, w_eps.detach(), w_hid.detach(), b_hid.detach(), w_head.detach(),
-            b_head.detach())
+            b_head.detach(), self.theta_fold(fl, theta))
         # sde / obs from the written path and their theta gradient (x is a constant here: the fused kernel
         # differentiated through it)
         th = theta.detach().contiguous()

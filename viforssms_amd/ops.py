@@ -154,15 +154,25 @@ class FlowShape:
         return self.Lout // (2 if self.stride2 else 1)
 
 
-def _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head) -> FlowParams:
-    return FlowParams(ptr(w_eps), ptr(w_hid), ptr(b_hid), ptr(bn_g), ptr(bn_b), ptr(w_head), ptr(b_head))
+def _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf=None) -> FlowParams:
+    """VissmFlowParams; tf = (theta [B, R], w_theta [R, H], b_theta [H]) is the theta branch's factorization
+    (theta_term = theta w_theta + b_theta), which the two-sample AR kernels fold into their layer-0 product."""
+    if tf is None:
+        return FlowParams(ptr(w_eps), ptr(w_hid), ptr(b_hid), ptr(bn_g), ptr(bn_b), ptr(w_head), ptr(b_head))
+    th, wt, bt = tf
+    _require_gpu(th, wt, bt)
+    if not (th.is_contiguous() and wt.is_contiguous() and bt.is_contiguous()) or th.shape[1] != wt.shape[0]:
+        raise _lib.VissmError("theta factors: contiguous theta [B, R], w_theta [R, H], b_theta [H] expected")
+    return FlowParams(ptr(w_eps), ptr(w_hid), ptr(b_hid), ptr(bn_g), ptr(bn_b), ptr(w_head), ptr(b_head),
+                      ptr(th), ptr(wt), ptr(bt), int(th.shape[1]))
 
 
 class MAFlowFn(torch.autograd.Function):
     """One IAF flow (IAF._create_flow, AR.py:50-85) -> (u_next, logsig)."""
 
     @staticmethod
-    def forward(ctx, shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head):
+    def forward(ctx, shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head,
+                tf=None):
         lib = _lib.load()
         _require_gpu(u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, win)
         dev = u.device
@@ -173,11 +183,12 @@ class MAFlowFn(torch.autograd.Function):
         if wsz == 0:
             check(-1, "vissm_flow_workspace_size")
         ws = _workspace(wsz, dev)
-        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf)
         check(lib.vissm_flow_fwd(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
                                  ptr(u_next), ptr(logsig), ptr(ws), wsz, _lib.stream_handle(dev)),
               "vissm_flow_fwd")
         ctx.shape = shape
+        ctx.tf = tf  # constants (no gradient flows through them: theta_term carries it)
         ctx.save_for_backward(win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
         return u_next, logsig
 
@@ -205,15 +216,15 @@ class MAFlowFn(torch.autograd.Function):
         grads = FlowGrads(*[ptr(t) for t in gw])
         wsz = lib.vissm_flow_workspace_size(ctypes.byref(d), 1)
         ws = _workspace(wsz, dev)
-        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, ctx.tf)
         check(lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
                                  ptr(g_next), ptr(g_ls), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws),
                                  wsz, _lib.stream_handle(dev)), "vissm_flow_bwd")
-        return (None, None, du, dC, dth, *gw)
+        return (None, None, du, dC, dth, *gw, None)
 
 
-def ma_flow(shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head):
-    return MAFlowFn.apply(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+def ma_flow(shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf=None):
+    return MAFlowFn.apply(shape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf)
 
 
 def ar_fused_supported(shape: FlowShape) -> bool:
@@ -222,7 +233,7 @@ def ar_fused_supported(shape: FlowShape) -> bool:
 
 
 def ar_last_flow_fused(shape: FlowShape, win, u, C, theta_term, theta, obs, obs_bin, obs_std: float, scale: float,
-                       w_eps, w_hid, b_hid, w_head, b_head):
+                       w_eps, w_hid, b_hid, w_head, b_head, tf=None):
     """The last AR(1) flow fused with its ELBO terms (vissm_flow_ar_elbo_fused): one backward-style pass that
     recomputes the flow's output x and differentiates loss = -scale sum_b (sde + obs + logsig) w.r.t. u, C,
     theta_term and the flow's weights (no autograd: the caller routes them; the theta dependence of sde goes
@@ -243,7 +254,7 @@ def ar_last_flow_fused(shape: FlowShape, win, u, C, theta_term, theta, obs, obs_
     dth = torch.empty_like(theta_term)
     gw = [torch.empty_like(t) for t in (w_eps, w_hid, b_hid, w_head, b_head)]
     grads = FlowGrads(ptr(gw[0]), ptr(gw[1]), ptr(gw[2]), None, None, ptr(gw[3]), ptr(gw[4]))
-    prm = _flow_params(w_eps, w_hid, b_hid, None, None, w_head, b_head)
+    prm = _flow_params(w_eps, w_hid, b_hid, None, None, w_head, b_head, tf)
     check(lib.vissm_flow_ar_elbo_fused(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
                                        ptr(theta), ptr(obs), ptr(obs_bin), float(obs_std), float(scale), ptr(x),
                                        ptr(logsig), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws), wsz,
