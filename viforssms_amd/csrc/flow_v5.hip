@@ -1498,6 +1498,25 @@ template <bool FZ>
 __device__ __forceinline__ void fence2() {
   if constexpr (VISSM_BWD2_FENCE == 1 || (VISSM_BWD2_FENCE == 2 && FZ)) fence();
 }
+#ifndef VISSM_BWD2_ELUE
+#define VISSM_BWD2_ELUE 0  // elu'(I_1) = min(2^x', 1) from the recompute's exp (kept in registers to the head
+                           // backward) instead of re-derived from I_1 (med3 + fma per element)
+#endif
+#ifndef VISSM_BWD2_DCMF
+#define VISSM_BWD2_DCMF 1  // the dC tile summed by a K = 32 MFMA over the pair's dA0 image fragments (a position
+                           // selection B operand) instead of fp32 VALU adds of the dA0 accumulators
+#endif
+#ifndef VISSM_BWD2_DTMF
+#define VISSM_BWD2_DTMF 0  // per-sample d theta accumulated for the whole item by a K = 32 MFMA against a one-hot
+                           // sample operand into a [h][16 samples] accumulator (16 VGPRs) instead of per-pair LDS
+                           // read-modify-writes of [S][DTH] rows (28 KB of LDS per block freed)
+#endif
+#ifndef VISSM_BWD2_DWT
+#define VISSM_BWD2_DWT 1  // dW_eps accumulated transposed ([h][tap]) by one K = 32 MFMA per row block whose B operand's
+                          // columns 8..15 carry one-hot sample columns: the same product also sums d theta for 8
+                          // samples, flushed to the LDS rows every fourth pair (4 MFMAs and 3 of 4 read-modify-writes
+                          // fewer per pair)
+#endif
 #ifndef VISSM_BWD2_PRIO
 #define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
 #endif
@@ -1535,7 +1554,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW2][2][2 * P * HP];  // [wave][slot][row 16 cb + position][64 h]
-  __shared__ float dthl[NW2][S][DTH];
+  __shared__ float dthl[NW2][VISSM_BWD2_DTMF ? 1 : S][DTH];
   __shared__ __attribute__((aligned(16))) float dths[NW2][4];
   __shared__ float carry[NW2][S][KP2];
   __shared__ float gsc[NW2][2][P];
@@ -1552,7 +1571,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
     for (int i = threadIdx.x; i < NW2 * S * P; i += NT2) (&zls[0][0][0])[i] = 0.f;
     for (int i = threadIdx.x; i < NW2 * S; i += NT2) (&zcar[0][0])[i] = 0.f;
   }
-  for (int i = threadIdx.x; i < NW2 * S * DTH; i += NT2) (&dthl[0][0][0])[i] = 0.f;
+  if constexpr (!VISSM_BWD2_DTMF)
+    for (int i = threadIdx.x; i < NW2 * S * DTH; i += NT2) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW2 * S * KP2; i += NT2) (&carry[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW2 * 2 * KP2 * QW2; i += NT2) (&dscr[0][0][0][0])[i] = 0.f;
   __syncthreads();
@@ -1568,12 +1588,14 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   const unsigned* whp = reinterpret_cast<const unsigned*>(&sh.cst[NH * HP]);  // (mu, r) bf16 pairs
 
   f4 dW[4][4], dWe[4], dWh[4];
+  f4 DT[4];  // VISSM_BWD2_DTMF: d theta of the group's 16 samples, [h][sample] (lane (g, c): sample c)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) dW[i][o] = f4{0.f, 0.f, 0.f, 0.f};
     dWe[i] = f4{0.f, 0.f, 0.f, 0.f};
     dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
+    DT[i] = f4{0.f, 0.f, 0.f, 0.f};
   }
   const int fwc = 16 * NH + 4 * KB;
   // d theta's ones operand, split by sample: B[k = 8g + jj][n = c] = 1 if position k belongs to the sample of
@@ -1581,6 +1603,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   bf8 ones_ab;
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) ones_ab[jj] = (__bf16)(((jj < 4) == (c < 8)) ? 1.f : 0.f);
+  // VISSM_BWD2_DCMF: B[k = 8g + jj][n = c] = 1 if k's position 4g + (jj & 3) is column n (either sample)
+  bf8 sel_p;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) sel_p[jj] = (__bf16)((4 * g + (jj & 3) == c) ? 1.f : 0.f);
 
   const float ldl = (!FZ && lane < nb) ? dls[b_lo + lane] : 0.f;
   float lt0 = 0.f, lt1 = 0.f, lis = 0.f;
@@ -1662,6 +1688,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       // ---- forward recompute of both samples (shared weight fragments)
       u2 i0p[2][4];
+      f4 E1[2][4];  // VISSM_BWD2_ELUE: elu'(I_1)
       float mu[2], rr[2];
       {
         f4 acc[2][4];
@@ -1720,6 +1747,14 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
           if (g == 3) X[cb][3][3] = 1.f;
+        if constexpr (VISSM_BWD2_ELUE) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) E1[cb][rb][r] = fminf(__builtin_amdgcn_exp2f(acc[cb][rb][r]), 1.f);
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const Fr8<NP> wf = wfrag(sh, fh + ks, lane);
@@ -1822,7 +1857,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r)
+              D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * (VISSM_BWD2_ELUE ? E1[cb][rb][r] : elu_d(X[cb][rb][r])) : 0.f;
           put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
         }
       }
@@ -1876,11 +1912,13 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int cb = 0; cb < 2; ++cb) dcn[cb] = mm<NP>(wc, chain_frag<NP>(D[cb], ks), dcn[cb]);
         }
       }
+      if constexpr (!VISSM_BWD2_DCMF) {
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
+          for (int r = 0; r < 4; ++r)
+            if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
+      }
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);  // dA0 -> slot 1
       if constexpr (DU) {
@@ -1896,20 +1934,58 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       // dW_eps and d theta from dA0's position-contracted fragments (K = 32)
       f4 dth4[4];
       {
+        // VISSM_BWD2_DTMF: B[k][n] = 1 if k's sample (jj >> 2: A, B) is group sample n
+        const unsigned one2 = 0x3F803F80u, sa = c == blv[0] ? one2 : 0u, sb = (two && c == blv[1]) ? one2 : 0u;
+        const bf8 selb = __builtin_bit_cast(bf8, u4{sa, sa, sb, sb});
         bf8 uaf;
         {
           const Fr4<NP> ua = ua_frag<NP>(uwin[w][0], 1, 0, g, c), ub = ua_frag<NP>(uwin[w][1], 1, 0, g, c);
           uaf = cat8(ua.h, ub.h);
         }
+        // VISSM_BWD2_DWT: one B operand for dW_eps^T (columns j < 8: the u windows) and the d theta of the pair's
+        // two samples (columns 8 + slot: one-hot by sample, slot = sample mod 8)
+        bf8 bcomb = uaf;
+        if constexpr (VISSM_BWD2_DWT) {
+          const unsigned ta_ = c - 8 == (blv[0] & 7) ? one2 : 0u, tb_ = (two && c - 8 == (blv[1] & 7)) ? one2 : 0u;
+          if (c >= 8) bcomb = __builtin_bit_cast(bf8, u4{ta_, ta_, tb_, tb_});
+        }
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
           const bf8 ta = tr_frag2(im1, hb, g, c);
-          dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
-          dWe[hb] = mfma32(uaf, ta, dWe[hb]);
+          if constexpr (VISSM_BWD2_DWT) {
+            dWe[hb] = mfma32(ta, bcomb, dWe[hb]);
+          } else {
+            if constexpr (VISSM_BWD2_DTMF) DT[hb] = mfma32(ta, selb, DT[hb]);
+            else dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
+            dWe[hb] = mfma32(uaf, ta, dWe[hb]);
+          }
+          if constexpr (VISSM_BWD2_DCMF) dCa[hb] = mfma32(ta, sel_p, dCa[hb]);
+        }
+      }
+      // VISSM_BWD2_DWT: the eight sample columns flushed into the per-sample d theta rows after every fourth pair
+      // and after the tile's last, then cleared
+      if constexpr (VISSM_BWD2_DWT) {
+        if ((bl & 7) == 6 || bl + 2 >= nb) {
+          const int smp = (bl & ~7) + c - 8;
+          if (c >= 8 && smp < nb) {
+            float* base = &dthl[w][smp][4 * g];
+            f4* dp[4];
+#pragma unroll
+            for (int hb = 0; hb < 4; ++hb)
+              dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
+            f4 o[4];
+#pragma unroll
+            for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
+#pragma unroll
+            for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dWe[hb];
+          }
+#pragma unroll
+          for (int hb = 0; hb < 4; ++hb)
+            if (c >= 8) dWe[hb] = f4{0.f, 0.f, 0.f, 0.f};
         }
       }
       // per-sample d theta read-modify-writes: lane c = 0 (sample A) and c = 8 (sample B)
-      if (c == 0 || (c == 8 && two)) {
+      if (!VISSM_BWD2_DTMF && !VISSM_BWD2_DWT && (c == 0 || (c == 8 && two))) {
         float* base = &dthl[w][c == 0 ? blv[0] : blv[1]][4 * g];
         f4* dp[4];
 #pragma unroll
@@ -1987,7 +2063,20 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + lane] = v;
       }
     }
-    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
+    if (!VISSM_BWD2_DTMF && lane < a.H)
+      dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
+  }
+  if constexpr (VISSM_BWD2_DTMF) {
+    if (c < nb) {
+      float* row = dth_slab + (static_cast<size_t>(chn) * a.B + b_lo + c) * a.H;
+#pragma unroll
+      for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = swz(16 * hb + 4 * g + r);
+          if (h < a.H) row[h] = DT[hb][r] * kLog2e;
+        }
+    }
   }
 
   // weight-gradient partials of this work item (the layout of bwd_kernel's)
@@ -1999,7 +2088,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 4 * g + r, h = swz(16 * hb + c);
-      if (j < a.k && h < H) ws[j * H + h] = dWe[hb][r] * kLog2e;
+      if constexpr (VISSM_BWD2_DWT) {  // dWe^T: lane column c = tap, rows h
+        const int ht = swz(16 * hb + 4 * g + r);
+        if (c < a.k && ht < H) ws[c * H + ht] = dWe[hb][r] * kLog2e;
+      } else if (j < a.k && h < H) ws[j * H + h] = dWe[hb][r] * kLog2e;
     }
   const int off_w = a.k * H, off_b = off_w + NH * H * H;
 #pragma unroll
