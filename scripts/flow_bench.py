@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--impls", default="fp32,bf16", help="flow precisions to time: fp32, bf16, bf16x3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="", help="run only this impl (for PMC passes)")
+    ap.add_argument("--fold", type=int, default=1, help="pass the theta branch's factors (theta_term = theta W + b, "
+                    "rank 3): the two-sample AR kernels fold them into the layer-0 product, as the training step does")
     args = ap.parse_args()
     lib = _lib.load()
     dev = torch.device("cuda", 0)
@@ -38,7 +40,9 @@ def main():
     r = lambda *s, sc=1.0: (torch.randn(*s, generator=g, device=dev) * sc).contiguous()
     u = r(B, L)
     C = r(1, sh.Lh, H, sc=0.3)
-    tt = r(B, H, sc=0.3)
+    th3, wt3, bt3 = r(B, 3, sc=0.5), r(3, H, sc=0.2), r(H, sc=0.1)
+    tt = torch.addmm(bt3, th3, wt3).contiguous()
+    tf = (th3, wt3, bt3) if args.fold else None
     w_eps, w_hid, b_hid = r(k, H, sc=0.3), r(nh, H, H, sc=0.15), r(nh, H, sc=0.1)
     bn_g, bn_b = (1 + r(nh, H, sc=0.1), r(nh, H, sc=0.1)) if nh > 1 else (None, None)
     w_head, b_head = r(H, 2, sc=0.2), r(2, sc=0.1)
@@ -68,7 +72,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             un, ls = MAFlowFn.apply(shp, None, ins[0], ins[1], ins[2], ins[3], ins[4], ins[5], extra[0], extra[1],
-                                    ins[6], ins[7])
+                                    ins[6], ins[7], tf)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             torch.autograd.backward([un, ls], [gnext, gls])
