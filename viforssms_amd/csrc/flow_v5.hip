@@ -2132,6 +2132,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #ifndef VISSM_THETA_FOLD
 #define VISSM_THETA_FOLD 1  // the two-sample AR kernels form the theta term in the layer-0 product (fold_ok)
 #endif
+#ifndef VISSM_FWD2_X2
+#define VISSM_FWD2_X2 1  // the bf16x2 forward (parity-precision modes) runs the two-sample kernel too
+#endif
 #ifndef VISSM_FWD2_REGW
 #define VISSM_FWD2_REGW 1
 #endif
@@ -2141,7 +2144,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // TF: the theta fold (VissmFlowParams.theta_rank): the theta term rides in the layer-0 product's K rows 16..31
 // (lane groups 2, 3 of the B operand: the sample's fragment thf[b][g - 2], loaded once per pair) instead of a
 // [64] theta_term row per sample and tile added to the C rows
-template <bool TF>
+// NP = 2: the bf16x2 forward (split weights w_hi x + w_lo x, bf16 activations; the parity-precision modes'
+// forward): hi planes register-resident, lo planes read from LDS per use
+template <bool TF, int NP>
 __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
@@ -2150,7 +2155,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
                                                                   float* __restrict__ u_next,
                                                                   float* __restrict__ ls_slab,
                                                                   const u4* __restrict__ thf) {
-  constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
+  constexpr int NH = 1, KB = 1, JB = 1;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][2][64];
   load_shared(sh, img, cst);
@@ -2177,10 +2182,18 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
 #pragma unroll
     for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
   }
-  // fragment f of the shared image, or its register copy (index i)
-  auto W = [&](int f, int i) -> bf8 {
-    if constexpr (VISSM_FWD2_REGW) return wr[i];
-    else return sh.img[f][0][lane];
+  // fragment f of the shared image, or its register copy (index i); NP = 2: with its lo plane from LDS
+  auto W = [&](int f, int i) -> Fr8<NP> {
+    Fr8<NP> r;
+    if constexpr (VISSM_FWD2_REGW) r.h = wr[i];
+    else r.h = sh.img[f][0][lane];
+    if constexpr (NP == 2) r.l = sh.img[f][1][lane];
+    return r;
+  };
+  // weight (A) x activation (B, bf16) product at the kernel's precision
+  auto mmw = [](const Fr8<NP>& a, const bf8& b, f4 cc) -> f4 {
+    if constexpr (NP == 2) cc = mfma32(a.l, b, cc);
+    return mfma32(a.h, b, cc);
   };
   const int nu = a.k + P;
   for (int bl = 0; bl < nb; bl += 2) {
@@ -2220,7 +2233,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       }
       f4 acc[2][4];
       {
-        bf8 uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c).h, u_frag<NP>(uwin[w][1], 1, 0, g, c).h};
+        bf8 uf[2] = {u_frag<1>(uwin[w][0], 1, 0, g, c).h, u_frag<1>(uwin[w][1], 1, 0, g, c).h};
         if constexpr (TF) {
           if (g >= 2) {
             uf[0] = tfr[0];
@@ -2229,9 +2242,9 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
         }
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
-          const bf8 wf = W(16 * NH + ob, 8 * NH + ob);
+          const Fr8<NP> wf = W(16 * NH + ob, 8 * NH + ob);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mfma32(wf, uf[cb], X[cb][ob]);
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, uf[cb], X[cb][ob]);
         }
       }
 #pragma unroll
@@ -2246,12 +2259,12 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf8 xf[2] = {chain_frag<NP>(X[0], ks).h, chain_frag<NP>(X[1], ks).h};
+        const bf8 xf[2] = {chain_frag<1>(X[0], ks).h, chain_frag<1>(X[1], ks).h};
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
-          const bf8 wf = W(ob * 2 + ks, ob * 2 + ks);
+          const Fr8<NP> wf = W(ob * 2 + ks, ob * 2 + ks);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mfma32(wf, xf[cb], acc[cb][ob]);
+          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, xf[cb], acc[cb][ob]);
         }
       }
 #pragma unroll
@@ -2266,9 +2279,9 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf8 wf = W(fh + ks, 8 * NH + 4 * KB + ks);
+        const Fr8<NP> wf = W(fh + ks, 8 * NH + 4 * KB + ks);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) d[cb] = mfma32(wf, chain_frag<NP>(X[cb], ks).h, d[cb]);
+        for (int cb = 0; cb < 2; ++cb) d[cb] = mmw(wf, chain_frag<1>(X[cb], ks).h, d[cb]);
       }
       if (g == 0 && c < nP) {
 #pragma unroll
@@ -2956,7 +2969,8 @@ static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
 
 // the two-sample forward covers the AR configurations' flow shape
 static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_FWD2 && d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
+  return VISSM_FWD2 && (d->precision == VISSM_PREC_BF16 || (VISSM_FWD2_X2 && d->precision == VISSM_PREC_BF16X2)) &&
+         d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
          d->k <= 16 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
 }
 
@@ -3068,12 +3082,12 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
   if (f2) {
-    if (fold)
-      hipLaunchKernelGGL(fwd2_kernel<true>, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next,
-                         ws.ls_slab, ws.thf);
-    else
-      hipLaunchKernelGGL(fwd2_kernel<false>, grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next,
-                         ws.ls_slab, ws.thf);
+#define FWD2_LAUNCH(TF_, NP_)                                                                                   \
+  hipLaunchKernelGGL((fwd2_kernel<TF_, NP_>), grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, \
+                     ws.ls_slab, ws.thf)
+    if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2); else FWD2_LAUNCH(false, 2); }
+    else { if (fold) FWD2_LAUNCH(true, 1); else FWD2_LAUNCH(false, 1); }
+#undef FWD2_LAUNCH
   } else if (np_of(d) == 2) {
     if (jb_of(d->k) == 1)
       hipLaunchKernelGGL((fwd_kernel<1, 1, 1, 2>), grid, dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp, ws.img, ws.cst, u_next,
