@@ -2132,6 +2132,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #ifndef VISSM_THETA_FOLD
 #define VISSM_THETA_FOLD 1  // the two-sample AR kernels form the theta term in the layer-0 product (fold_ok)
 #endif
+#ifndef VISSM_FWD2N
+#define VISSM_FWD2N 1  // the three-hidden-layer forward (LV / FHN heads, k <= 32) on the two-sample kernel
+#endif
 #ifndef VISSM_FWD2_X2
 #define VISSM_FWD2_X2 1  // the bf16x2 forward (parity-precision modes) runs the two-sample kernel too
 #endif
@@ -2146,7 +2149,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // [64] theta_term row per sample and tile added to the C rows
 // NP = 2: the bf16x2 forward (split weights w_hi x + w_lo x, bf16 activations; the parity-precision modes'
 // forward): hi planes register-resident, lo planes read from LDS per use
-template <bool TF, int NP>
+// NH / JB: one hidden layer (AR) or three with the BN affine folded (LV / SV / FHN heads: stride-2 head with the
+// pass-through of the even outputs and the fused pair swap), k <= 32 (one layer-0 K block)
+template <bool TF, int NP, int NH, int JB>
 __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
@@ -2155,7 +2160,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
                                                                   float* __restrict__ u_next,
                                                                   float* __restrict__ ls_slab,
                                                                   const u4* __restrict__ thf) {
-  constexpr int NH = 1, KB = 1, JB = 1;
+  constexpr int KB = 1;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][2][64];
   load_shared(sh, img, cst);
@@ -2195,7 +2200,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
     if constexpr (NP == 2) cc = mfma32(a.l, b, cc);
     return mfma32(a.h, b, cc);
   };
-  const int nu = a.k + P;
+  const int nu = a.s * P + a.k;  // u entries a unit reads (<= 64)
   for (int bl = 0; bl < nb; bl += 2) {
     const bool two = bl + 1 < nb;
     const int bv[2] = {b_lo + bl, b_lo + (two ? bl + 1 : bl)};
@@ -2206,7 +2211,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       for (int cb = 0; cb < 2; ++cb) tfr[cb] = __builtin_bit_cast(bf8, thf[2 * static_cast<size_t>(bv[cb]) + (g & 1)]);
     }
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
-      const int nP = min(P, m_hi - m0), t0 = m0;
+      const int nP = min(P, m_hi - m0), t0 = a.s * m0;
       f4 X[2][4];
       {
         float uv[2];
@@ -2233,7 +2238,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       }
       f4 acc[2][4];
       {
-        bf8 uf[2] = {u_frag<1>(uwin[w][0], 1, 0, g, c).h, u_frag<1>(uwin[w][1], 1, 0, g, c).h};
+        bf8 uf[2] = {u_frag<1>(uwin[w][0], a.s, 0, g, c).h, u_frag<1>(uwin[w][1], a.s, 0, g, c).h};
         if constexpr (TF) {
           if (g >= 2) {
             uf[0] = tfr[0];
@@ -2248,33 +2253,39 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
         }
       }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
+      for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
-        if (g == 3) X[cb][3][3] = 1.f;
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) acc[cb][ob] = f4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int l = 0; l < NH; ++l) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf8 xf[2] = {chain_frag<1>(X[0], ks).h, chain_frag<1>(X[1], ks).h};
+        for (int cb = 0; cb < 2; ++cb) {
+          if (g == 3) X[cb][3][3] = 1.f;  // the ones row: bias of layer l
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-          const Fr8<NP> wf = W(ob * 2 + ks, ob * 2 + ks);
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, xf[cb], acc[cb][ob]);
+          for (int ob = 0; ob < 4; ++ob) acc[cb][ob] = f4{0.f, 0.f, 0.f, 0.f};
         }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf8 xf[2] = {chain_frag<1>(X[0], ks).h, chain_frag<1>(X[1], ks).h};
+#pragma unroll
+          for (int ob = 0; ob < 4; ++ob) {
+            const Fr8<NP> wf = W(l * 8 + ob * 2 + ks, l * 8 + ob * 2 + ks);
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, xf[cb], acc[cb][ob]);
+          }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
       }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+      for (int cb = 0; cb < 2; ++cb)
         if (g == 3) X[cb][3][3] = 1.f;
-      }
       const int fh = 16 * NH + 4 * KB + 2 * JB;
       f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -2288,8 +2299,13 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
         for (int cb = 0; cb < 2; ++cb) {
           if (cb == 1 && !two) break;
           const float sg = softplus_fast(d[cb][1]) + 1e-10f;
-          const int o = t0 + c;
-          u_next[static_cast<size_t>(bv[cb]) * a.Lout + o] = uwin[w][cb][c + a.k] * sg + d[cb][0];
+          const int oq = a.s * c + (a.s - 1), o = t0 + oq;
+          float* ob = u_next + static_cast<size_t>(bv[cb]) * a.Lout;
+          ob[a.swap_out ? (o ^ 1) : o] = uwin[w][cb][oq + a.k] * sg + d[cb][0];
+          if (a.s == 2) {  // the even outputs pass through (lotka_volterra_partial.py:97-104)
+            const int oe = t0 + 2 * c;
+            ob[a.swap_out ? (oe ^ 1) : oe] = uwin[w][cb][2 * c + a.k];
+          }
           if (o >= a.Lout - a.n_logsig) ls[cb] += VISSM_FWD_HWLOG ? __builtin_amdgcn_logf(sg) * kLn2 : logf(sg);
         }
       }
@@ -2969,9 +2985,10 @@ static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
 
 // the two-sample forward covers the AR configurations' flow shape
 static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_FWD2 && (d->precision == VISSM_PREC_BF16 || (VISSM_FWD2_X2 && d->precision == VISSM_PREC_BF16X2)) &&
-         d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
-         d->k <= 16 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
+  if (!VISSM_FWD2 || d->H > kMaxH || d->n_win != 1 || g.S != S || d->k > 32) return false;
+  if (d->n_hidden == 1) return !d->bn && !d->stride2 && !d->swap_out && (d->precision == VISSM_PREC_BF16 ||
+                                                                        (VISSM_FWD2_X2 && d->precision == VISSM_PREC_BF16X2));
+  return VISSM_FWD2N && d->n_hidden == 3 && d->precision == VISSM_PREC_BF16;
 }
 
 }  // namespace VISSM_FLOW5_NS
@@ -3043,7 +3060,7 @@ size_t VISSM_FLOW5_API(flow5_workspace_size)(const VissmFlowDesc* d, int backwar
 // the layer-0 product free
 static bool fold_ok(const VissmFlowDesc* d, const VissmFlowParams* w) {
   return VISSM_THETA_FOLD && w->theta_rank >= 1 && w->theta_rank <= 5 && w->theta_x && w->w_theta && w->b_theta &&
-         d->k <= kFoldRow;
+         d->k <= kFoldRow && d->n_hidden == 1;
 }
 
 // padded C (+ b_theta when folding) and either the padded theta term or the theta fold's B-operand rows
@@ -3082,11 +3099,14 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
   if (f2) {
-#define FWD2_LAUNCH(TF_, NP_)                                                                                   \
-  hipLaunchKernelGGL((fwd2_kernel<TF_, NP_>), grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, \
-                     ws.ls_slab, ws.thf)
-    if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2); else FWD2_LAUNCH(false, 2); }
-    else { if (fold) FWD2_LAUNCH(true, 1); else FWD2_LAUNCH(false, 1); }
+#define FWD2_LAUNCH(TF_, NP_, NH_, JB_)                                                                           \
+  hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_>), grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, \
+                     u_next, ws.ls_slab, ws.thf)
+    const int jb = jb_of(d->k);
+    if (d->n_hidden == 3) { if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1); else FWD2_LAUNCH(false, 1, 3, 2); }
+    else if (jb == 2) { if (np_of(d) == 2) FWD2_LAUNCH(false, 2, 1, 2); else FWD2_LAUNCH(false, 1, 1, 2); }
+    else if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2, 1, 1); else FWD2_LAUNCH(false, 2, 1, 1); }
+    else { if (fold) FWD2_LAUNCH(true, 1, 1, 1); else FWD2_LAUNCH(false, 1, 1, 1); }
 #undef FWD2_LAUNCH
   } else if (np_of(d) == 2) {
     if (jb_of(d->k) == 1)
