@@ -329,8 +329,9 @@ def measure(args, ctx, dev, parity_line: bool):
         for name, mode, note in (
                 ("bf16x2f", _lib.VISSM_PREC_BF16X2F,
                  "forward flow products with split-bf16 weights (w_hi x + w_lo x: the weights' rounding, coherent "
-                 "over a path, removed) and bf16 activations, backward products bf16: per-sample ELBO within 1e-4 "
-                 "of the float64 oracle, gradient at bf16 accuracy (tests/test_gpu_config_parity.py)"),
+                 "over a path, removed) and bf16 activations, backward products bf16 (the last flow fused with the "
+                 "ELBO terms, its recompute on split weights): per-sample ELBO within 1e-4 of the float64 oracle, "
+                 "gradient at bf16 accuracy (tests/test_gpu_config_parity.py, tests/test_gpu_fused.py)"),
                 ("bf16x3f", _lib.VISSM_PREC_BF16X3F,
                  "forward flow products bf16x3 (the values reaching the ELBO), backward products bf16: per-sample "
                  "ELBO within 1e-4 of the float64 oracle, gradient at bf16 accuracy (tests/test_gpu_config_parity.py)"),
@@ -343,7 +344,8 @@ def measure(args, ctx, dev, parity_line: bool):
             f_ms, f_n, _ = px_prof[_lib.PROF_FLOW_FWD]
             px.append({"dtype": name, "value": world * args.B * args.M * args.steps / px_elapsed,
                        "ms_per_step": px_elapsed / args.steps * 1e3, "flow_bwd_avg_ms": b_ms / max(b_n, 1),
-                       "flow_fwd_avg_ms": f_ms / max(f_n, 1), "note": note})
+                       "flow_fwd_avg_ms": f_ms / max(f_n, 1),
+                       "last_flow_fused": bool(px_prof[_lib.PROF_FLOW_FUSED][1]), "note": note})
         model.engine.precision = prec
 
     B, T, k, H, nh, nf, D, bn = args.B, args.M, args.k, 50, meta["nh"], meta["n_flows"], meta["D"], meta["bn"]

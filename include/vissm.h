@@ -44,7 +44,8 @@ extern "C" {
 #define VISSM_PREC_BF16 1     /* bf16 MFMA operands, fp32 accumulation */
 #define VISSM_PREC_BF16X3 2   /* split-bf16 (hi/lo) MFMA operands: ~fp32 products */
 #define VISSM_PREC_BF16X2 3   /* forward only: split-bf16 weights, bf16 activations (two MFMAs per product);
-                                 vissm_flow_bwd / vissm_flow_ar_elbo_fused reject it */
+                                 vissm_flow_bwd rejects it; vissm_flow_ar_elbo_fused takes it for k <= 8 on one
+                                 window (its recompute -- x, log sigma -- on split weights, backward products bf16) */
 
 const char* vissm_last_error(void);
 int vissm_version(void);

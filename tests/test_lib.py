@@ -56,7 +56,10 @@ def test_bf16x2_is_forward_only_without_gpu():
     rc = lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(w), p, p, None, p, p, p, p, p, p, ctypes.byref(gr), p, 64,
                             None)
     assert rc < 0 and b"forward-only" in lib.vissm_last_error()
-    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)) == 0
+    # the fused last AR flow takes it at the two-sample kernel's shape (split-weight recompute, bf16 backward products)
+    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)) == 1
+    d33 = _lib.FlowDesc(4, 60, 20, 50, 1, 0, 0, 0, 32, 1, _lib.VISSM_PREC_BF16X2, 0)   # k = 20: not that shape
+    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d33)) == 0
     assert set(_lib.HOST_MODES) <= set(_lib.TRAIN_PRECISIONS.values())
 
 
@@ -139,3 +142,19 @@ def test_softplus_ildj_matches_oracle():
         (gr,) = torch.autograd.grad(ref, [yt])
         assert abs(v - ref.item()) <= 1e-5 * max(1, abs(ref.item()))
         assert abs(g.value - gr.item()) <= 1e-4 * max(1, abs(gr.item()))
+
+
+def test_abi_struct_layouts_match_ctypes():
+    """The ctypes mirrors of VissmFlowDesc / VissmFlowParams / VissmFlowGrads (viforssms_amd/_lib.py) have the C
+    compiler's sizes and last-field offsets (include/vissm.h; round 3 appended the theta-fold fields)."""
+    from viforssms_amd import _lib
+    lib = ctypes.CDLL(HOSTCHECK)
+    f = lib.vissm_host_abi_layout
+    f.restype = None
+    f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+    for which, (cls, last) in enumerate([(_lib.FlowDesc, "chunk_tiles"), (_lib.FlowParams, "theta_rank"),
+                                         (_lib.FlowGrads, "b_head")]):
+        out = (ctypes.c_size_t * 2)()
+        f(which, out)
+        assert out[0] == ctypes.sizeof(cls), (cls.__name__, out[0], ctypes.sizeof(cls))
+        assert out[1] == getattr(cls, last).offset, (cls.__name__, last)

@@ -144,7 +144,8 @@ int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, c
   int rc = validate(d);
   if (rc) return rc;
   VISSM_CHECK_ARG(flow5_ar_fused_supports(d),
-                  "flow_ar_elbo_fused: needs bf16 / bf16x3, one hidden layer, no BN, stride 1, k <= 32");
+                  "flow_ar_elbo_fused: needs bf16 / bf16x3 (k <= 32) or bf16x2 (k <= 8, one window), one hidden layer, no BN, "
+                  "stride 1");
   VISSM_CHECK_ARG(w && u && C && theta_term && theta && obs && obs_bin && x && logsig && du && dC && dtheta_term && gr,
                   "flow_ar_elbo_fused: null pointer");
   VISSM_CHECK_ARG(gr->w_eps && gr->w_hid && gr->b_hid && gr->w_head && gr->b_head, "flow_ar_elbo_fused: null grad");

@@ -1517,6 +1517,12 @@ __device__ __forceinline__ void fence2() {
                           // samples, flushed to the LDS rows every fourth pair (4 MFMAs and 3 of 4 read-modify-writes
                           // fewer per pair)
 #endif
+#ifndef VISSM_BWD2_FZLS
+#define VISSM_BWD2_FZLS 0  // fused variant: the per-sample log sigma sums through two padding rows of the dA0 image into
+                           // the merged dW_eps / d theta product instead of per-pair LDS read-modify-writes of [S][16]
+                           // column sums (no change at bf16, A/B; always on in the split-weight recompute variant, whose
+                           // lo weight planes take that LDS)
+#endif
 #ifndef VISSM_BWD2_PRIO
 #define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
 #endif
@@ -1541,7 +1547,10 @@ __device__ __forceinline__ bf8 tr_frag2(const __bf16* img, int hb, int g, int c)
   return cat8(tr_read(img, hb, g, c), tr_read(img + P * HP, hb, g, c));
 }
 
-template <bool FZ, bool DU, bool TF>
+// NPR = 2 (fused variant only, VISSM_PREC_BF16X2): the forward recompute -- the values that reach the ELBO through
+// x and log sigma -- on split weights (w_hi u + w_lo u, the bf16x2 forward's products; lo planes of its 14 fragments
+// in LDS), the backward products bf16
+template <bool FZ, bool DU, bool TF, int NPR = 1>
 __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                       const float* __restrict__ tht, const float* __restrict__ gout,
                                                       const float* __restrict__ dls, const bf8* __restrict__ img,
@@ -1561,14 +1570,28 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   __shared__ float uwin[NW2][2][64];
   __shared__ float gwin[NW2][2][P];
   __shared__ float dscr[NW2][2][KP2][QW2];
-  __shared__ float zls[FZ ? NW2 : 1][FZ ? S : 1][P];
+  constexpr bool ZLS = FZ && !VISSM_BWD2_FZLS && NPR == 1;  // per-column log sigma sums in LDS
+  static_assert(!FZ || ZLS || VISSM_BWD2_DWT, "the log sigma sums without LDS ride in the merged dW_eps / d theta product");
+  __shared__ float zls[ZLS ? NW2 : 1][ZLS ? S : 1][P];
+  __shared__ bf8 slo[NPR == 2 ? 14 : 1][64];  // NPR = 2: lo planes of WF 0..7, WE 0..3, WH 0..1
   __shared__ float zcar[FZ ? NW2 : 1][FZ ? S : 1];
-  load_shared<NH, KB, JB, NP, NT2>(sh, img, cst);
+  if constexpr (NPR == 2) {  // the image holds [frag][hi, lo][lane]: hi planes to sh, the recompute's lo planes to slo
+    constexpr int NFR = Shared<NH, KB, JB, NP>::NFR;
+    for (int i = threadIdx.x; i < NFR * 64; i += NT2) sh.img[i >> 6][0][i & 63] = img[((i >> 6) * 2) * 64 + (i & 63)];
+    for (int i = threadIdx.x; i < 14 * 64; i += NT2) {
+      const int j = i >> 6, f = j < 8 ? j : (j < 12 ? 16 * NH + (j - 8) : 16 * NH + 4 * KB + 2 * JB + (j - 12));
+      slo[j][i & 63] = img[(f * 2 + 1) * 64 + (i & 63)];
+    }
+    for (int i = threadIdx.x; i < Shared<NH, KB, JB, NP>::NCST; i += NT2) sh.cst[i] = cst[i];
+  } else {
+    load_shared<NH, KB, JB, NP, NT2>(sh, img, cst);
+  }
   if constexpr (VISSM_BWD2_PRIO == 1) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
   }
   if constexpr (FZ) {
-    for (int i = threadIdx.x; i < NW2 * S * P; i += NT2) (&zls[0][0][0])[i] = 0.f;
+    if constexpr (ZLS)
+      for (int i = threadIdx.x; i < NW2 * S * P; i += NT2) (&zls[0][0][0])[i] = 0.f;
     for (int i = threadIdx.x; i < NW2 * S; i += NT2) (&zcar[0][0])[i] = 0.f;
   }
   if constexpr (!VISSM_BWD2_DTMF)
@@ -1704,7 +1727,11 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int ob = 0; ob < 4; ++ob) {
           const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], X[cb][ob]);
+          for (int cb = 0; cb < 2; ++cb) {
+            acc[cb][ob] = X[cb][ob];
+            if constexpr (NPR == 2) acc[cb][ob] = mfma32(slo[8 + ob][lane], uf[cb].h, acc[cb][ob]);
+            acc[cb][ob] = mm<NP>(wf, uf[cb], acc[cb][ob]);
+          }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
@@ -1726,7 +1753,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int ob = 0; ob < 4; ++ob) {
             const Fr8<NP> wf = wfrag(sh, ob * 2 + ks, lane);
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, xf[cb], acc[cb][ob]);
+            for (int cb = 0; cb < 2; ++cb) {
+              if constexpr (NPR == 2) acc[cb][ob] = mfma32(slo[ob * 2 + ks][lane], xf[cb].h, acc[cb][ob]);
+              acc[cb][ob] = mm<NP>(wf, xf[cb], acc[cb][ob]);
+            }
           }
         }
 #pragma unroll
@@ -1759,7 +1789,11 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int ks = 0; ks < 2; ++ks) {
           const Fr8<NP> wf = wfrag(sh, fh + ks, lane);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) d[cb] = mm<NP>(wf, chain_frag<NP>(X[cb], ks), d[cb]);
+          for (int cb = 0; cb < 2; ++cb) {
+            const Fr8<NP> xk = chain_frag<NP>(X[cb], ks);
+            if constexpr (NPR == 2) d[cb] = mfma32(slo[12 + ks][lane], xk.h, d[cb]);
+            d[cb] = mm<NP>(wf, xk, d[cb]);
+          }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1771,6 +1805,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       // ---- head backward, per sample
       const bool pv = c < nP;
       float sig[2], gmu[2], gr[2];
+      float lsv[2] = {0.f, 0.f};  // fused variant without the LDS column sums: the output columns' log sigma
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         sig[cb] = softplus_fast(rr[cb]) + 1e-10f;
@@ -1801,9 +1836,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the rest of the unit reads
             if (pv && (cb == 0 || two)) {
               if constexpr (!(VISSM_BWD2_FZDIAG & 1)) fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
-              if constexpr (!(VISSM_BWD2_FZDIAG & 2)) zls[w][bl2][c] += lsg;
+              if constexpr (!(VISSM_BWD2_FZDIAG & 2) && ZLS) zls[w][bl2][c] += lsg;
             }
           }
+          if constexpr (!ZLS) lsv[cb] = (pv && (cb == 0 || two)) ? lsg : 0.f;
           if (lane == PO - 1 && (nP == PO || discard) && (cb == 0 || two)) zcar[w][bl2] = x;
         } else {
           gmu[cb] = pv ? gwin[w][cb][c] : 0.f;
@@ -1918,6 +1954,16 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
+      }
+      if constexpr (FZ && !ZLS) {
+        // the log sigma of the pair's output columns rides in two padding rows of the dA0 image (register (3, 1):
+        // row 49 = unit 52 <- hi, row 53 = unit 53 <- lo of a split-bf16 pair), so the merged dW_eps / d theta
+        // product sums it per sample with d theta (its other outputs there are discarded padding units)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float hi = bf16_hi(lsv[cb]);
+          D[cb][3][1] = g == 0 ? hi : (g == 1 ? lsv[cb] - hi : 0.f);
+        }
       }
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);  // dA0 -> slot 1
@@ -2049,8 +2095,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   if constexpr (FZ) {
     if (lane < nb) {
       float v = 0.f;
+      if constexpr (!ZLS) {
+        v = dthl[w][lane][49] + dthl[w][lane][53];
+      } else {
 #pragma unroll
-      for (int cc = 0; cc < P; ++cc) v += zls[w][lane][cc];
+        for (int cc = 0; cc < P; ++cc) v += zls[w][lane][cc];
+      }
       fz.lsl[static_cast<size_t>(chn) * a.B + b_lo + lane] = v;
     }
   }
@@ -2135,6 +2185,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #ifndef VISSM_FWD2N
 #define VISSM_FWD2N 1  // the three-hidden-layer forward (LV / FHN heads, k <= 32) on the two-sample kernel
 #endif
+#ifndef VISSM_FWD2_K64
+#define VISSM_FWD2_K64 1  // and for 32 < k <= 64 at stride 1 (SV: two layer-0 K blocks, 128-entry u window)
+#endif
 #ifndef VISSM_FWD2_X2
 #define VISSM_FWD2_X2 1  // the bf16x2 forward (parity-precision modes) runs the two-sample kernel too
 #endif
@@ -2160,9 +2213,9 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
                                                                   float* __restrict__ u_next,
                                                                   float* __restrict__ ls_slab,
                                                                   const u4* __restrict__ thf) {
-  constexpr int KB = 1;
+  constexpr int KB = (JB + 1) / 2;  // layer-0 K blocks (k > 32: two, a 128-entry u window)
   __shared__ Shared<NH, KB, JB, NP> sh;
-  __shared__ float uwin[NW][2][64];
+  __shared__ float uwin[NW][2][64 * KB];
   load_shared(sh, img, cst);
   if constexpr (VISSM_FWD_PRIO == 3) {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
@@ -2200,7 +2253,10 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
     if constexpr (NP == 2) cc = mfma32(a.l, b, cc);
     return mfma32(a.h, b, cc);
   };
-  const int nu = a.s * P + a.k;  // u entries a unit reads (<= 64)
+  // one hidden layer: the AR shape (stride 1, no swap: fwd2_ok) as compile-time constants
+  const int ss = NH == 1 ? 1 : a.s;
+  const bool swp = NH == 1 ? false : a.swap_out != 0;
+  const int nu = ss * P + a.k;  // u entries a unit reads (<= 64 KB)
   for (int bl = 0; bl < nb; bl += 2) {
     const bool two = bl + 1 < nb;
     const int bv[2] = {b_lo + bl, b_lo + (two ? bl + 1 : bl)};
@@ -2211,12 +2267,15 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
       for (int cb = 0; cb < 2; ++cb) tfr[cb] = __builtin_bit_cast(bf8, thf[2 * static_cast<size_t>(bv[cb]) + (g & 1)]);
     }
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
-      const int nP = min(P, m_hi - m0), t0 = a.s * m0;
+      const int nP = min(P, m_hi - m0), t0 = ss * m0;
       f4 X[2][4];
       {
-        float uv[2];
+        float uv[2][KB];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) uv[cb] = lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane, a.L)] : 0.f;
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < KB; ++i)
+            uv[cb][i] = 64 * i + lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + 64 * i + lane, a.L)] : 0.f;
         const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
         f4 cr[4], tr[2][4];
 #pragma unroll
@@ -2231,25 +2290,29 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          uwin[w][cb][lane] = uv[cb];
+#pragma unroll
+          for (int i = 0; i < KB; ++i) uwin[w][cb][64 * i + lane] = uv[cb][i];
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) X[cb][rb] = TF ? cr[rb] : cr[rb] + tr[cb][rb];
         }
       }
       f4 acc[2][4];
       {
-        bf8 uf[2] = {u_frag<1>(uwin[w][0], a.s, 0, g, c).h, u_frag<1>(uwin[w][1], a.s, 0, g, c).h};
-        if constexpr (TF) {
-          if (g >= 2) {
-            uf[0] = tfr[0];
-            uf[1] = tfr[1];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          bf8 uf[2] = {u_frag<1>(uwin[w][0], ss, kb, g, c).h, u_frag<1>(uwin[w][1], ss, kb, g, c).h};
+          if constexpr (TF) {
+            if (g >= 2) {
+              uf[0] = tfr[0];
+              uf[1] = tfr[1];
+            }
           }
-        }
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-          const Fr8<NP> wf = W(16 * NH + ob, 8 * NH + ob);
+          for (int ob = 0; ob < 4; ++ob) {
+            const Fr8<NP> wf = W(16 * NH + 4 * kb + ob, 8 * NH + 4 * kb + ob);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, uf[cb], X[cb][ob]);
+            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
+          }
         }
       }
 #pragma unroll
@@ -2299,12 +2362,12 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
         for (int cb = 0; cb < 2; ++cb) {
           if (cb == 1 && !two) break;
           const float sg = softplus_fast(d[cb][1]) + 1e-10f;
-          const int oq = a.s * c + (a.s - 1), o = t0 + oq;
+          const int oq = ss * c + (ss - 1), o = t0 + oq;
           float* ob = u_next + static_cast<size_t>(bv[cb]) * a.Lout;
-          ob[a.swap_out ? (o ^ 1) : o] = uwin[w][cb][oq + a.k] * sg + d[cb][0];
-          if (a.s == 2) {  // the even outputs pass through (lotka_volterra_partial.py:97-104)
+          ob[swp ? (o ^ 1) : o] = uwin[w][cb][oq + a.k] * sg + d[cb][0];
+          if (ss == 2) {  // the even outputs pass through (lotka_volterra_partial.py:97-104)
             const int oe = t0 + 2 * c;
-            ob[a.swap_out ? (oe ^ 1) : oe] = uwin[w][cb][2 * c + a.k];
+            ob[swp ? (oe ^ 1) : oe] = uwin[w][cb][2 * c + a.k];
           }
           if (o >= a.Lout - a.n_logsig) ls[cb] += VISSM_FWD_HWLOG ? __builtin_amdgcn_logf(sg) * kLn2 : logf(sg);
         }
@@ -2915,7 +2978,8 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
   a.dcb = g.dcb;
-  a.dc16 = (VISSM_BWD_DC16 && !g.dcb && d->n_win == 1 && (d->precision == VISSM_PREC_BF16)) ? 1 : 0;
+  a.dc16 = (VISSM_BWD_DC16 && !g.dcb && d->n_win == 1 &&
+            (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2)) ? 1 : 0;
   a.ncu = device_cus();
   return a;
 }
@@ -2968,6 +3032,9 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowPar
   }
 }
 
+#ifndef VISSM_BWD2_X2
+#define VISSM_BWD2_X2 1  // the fused last flow at VISSM_PREC_BF16X2 (bf16x2f): split-weight recompute in bwd2_kernel
+#endif
 // the two-sample backward covers the AR configurations' flow shape
 static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
   return VISSM_BWD2 && d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
@@ -2985,7 +3052,8 @@ static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
 
 // the two-sample forward covers the AR configurations' flow shape
 static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  if (!VISSM_FWD2 || d->H > kMaxH || d->n_win != 1 || g.S != S || d->k > 32) return false;
+  if (!VISSM_FWD2 || d->H > kMaxH || d->n_win != 1 || g.S != S || d->k > 64) return false;
+  if (d->k > 32 && (d->n_hidden != 3 || d->stride2 || !VISSM_FWD2_K64)) return false;  // two K blocks: SV's shape
   if (d->n_hidden == 1) return !d->bn && !d->stride2 && !d->swap_out && (d->precision == VISSM_PREC_BF16 ||
                                                                         (VISSM_FWD2_X2 && d->precision == VISSM_PREC_BF16X2));
   return VISSM_FWD2N && d->n_hidden == 3 && d->precision == VISSM_PREC_BF16;
@@ -3103,7 +3171,12 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_>), grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, \
                      u_next, ws.ls_slab, ws.thf)
     const int jb = jb_of(d->k);
-    if (d->n_hidden == 3) { if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1); else FWD2_LAUNCH(false, 1, 3, 2); }
+    if (d->n_hidden == 3) {
+      if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1);
+      else if (jb == 2) FWD2_LAUNCH(false, 1, 3, 2);
+      else if (jb == 3) FWD2_LAUNCH(false, 1, 3, 3);
+      else FWD2_LAUNCH(false, 1, 3, 4);
+    }
     else if (jb == 2) { if (np_of(d) == 2) FWD2_LAUNCH(false, 2, 1, 2); else FWD2_LAUNCH(false, 1, 1, 2); }
     else if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2, 1, 1); else FWD2_LAUNCH(false, 2, 1, 1); }
     else { if (fold) FWD2_LAUNCH(true, 1, 1, 1); else FWD2_LAUNCH(false, 1, 1, 1); }
@@ -3201,8 +3274,11 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
 
 // ---- the last AR(1) flow fused with its ELBO terms (vissm_flow_ar_elbo_fused) ----
 bool VISSM_FLOW5_API(flow5_ar_fused_supports)(const VissmFlowDesc* d) {
-  return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && d->n_hidden == 1 && !d->bn &&
-         !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH && d->n_win >= 1;
+  const bool shape = d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH &&
+                     d->n_win >= 1;
+  if (d->precision == VISSM_PREC_BF16X2)  // split-weight recompute: the two-sample kernel's shape only
+    return VISSM_BWD2_X2 && shape && d->k <= KP2 && d->n_win == 1;
+  return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && shape;
 }
 
 size_t VISSM_FLOW5_API(flow5_ar_fused_workspace_size)(const VissmFlowDesc* d) {
@@ -3230,7 +3306,8 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
                   "flow_ar_elbo_fused: workspace too small");
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
-  const bool b2 = bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
+  const bool x2 = d->precision == VISSM_PREC_BF16X2;
+  const bool b2 = x2 || bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
   launch_prep(d, w, ws, fold, st);
   launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_fused_prep");
@@ -3248,11 +3325,12 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(VISSM_PROF_FLOW_FUSED, st);
   if (b2) {
-#define BWD2F_LAUNCH(TF_)                                                                                            \
-  hipLaunchKernelGGL((bwd2_kernel<true, true, TF_>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u, ws.Cp, \
-                     ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img, ws.cst,    \
-                     du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, fz)
-    if (fold) BWD2F_LAUNCH(true); else BWD2F_LAUNCH(false);
+#define BWD2F_LAUNCH(TF_, NPR_)                                                                                      \
+  hipLaunchKernelGGL((bwd2_kernel<true, true, TF_, NPR_>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u,   \
+                     ws.Cp, ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img,     \
+                     ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, fz)
+    if (x2) { if (fold) BWD2F_LAUNCH(true, 2); else BWD2F_LAUNCH(false, 2); }
+    else { if (fold) BWD2F_LAUNCH(true, 1); else BWD2F_LAUNCH(false, 1); }
 #undef BWD2F_LAUNCH
   } else
     FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,

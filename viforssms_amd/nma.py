@@ -428,8 +428,11 @@ class Engine:
         md = self.mdef
         fl = self.flows[-1]
         L = md.kernel_ext - (md.n_flows - 1) * md.k
+        # bf16x2f: the fused kernel recomputes the flow on split weights (the bf16x2 forward's products: x and log
+        # sigma at that precision) and runs its backward products at bf16 (VISSM_PREC_BF16X2 on the fused entry)
+        prec = _lib.VISSM_PREC_BF16X2 if self.precision == _lib.VISSM_PREC_BF16X2F else self.precision
         return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
-                         swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
+                         swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=prec,
                          chunk_tiles=self.chunk_tiles)
 
     def theta_fold(self, fl: IAF, theta: torch.Tensor):
@@ -459,8 +462,8 @@ class Engine:
 
     def fused_ok(self, batch: Batch, B: int) -> bool:
         """The step can run the last flow fused with the AR(1) ELBO (bf16 / bf16x3 matrix-core kernels)."""
-        if (self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or self.precision in _lib.HOST_MODES
-                or not self.fuse_last):
+        if (self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or not self.fuse_last
+                or (self.precision in _lib.HOST_MODES and self.precision != _lib.VISSM_PREC_BF16X2F)):
             return False
         return ar_fused_supported(self._last_shape(batch, B))
 
@@ -482,8 +485,9 @@ class Engine:
             Lh = L - md.k
             C = fl.conv_shared(F, Lh, 1)
             tt = fl.theta_term(theta)
+            pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
-                              swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=self.precision,
+                              swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
                               chunk_tiles=self.chunk_tiles)
             u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta))
             lq = lq - ls
