@@ -445,13 +445,17 @@ class Engine:
         return fl.theta_factors(theta)
 
     def feature_gemm(self) -> Optional[str]:
-        """How the window-shared conv over features runs: split-bf16 products ("x3") at the bf16 training
-        precisions where that GEMM is large (LV: the time-mixing features have kernel_ext - 1 channels), fp32
-        otherwise (None).  VISSM_FEATURE_GEMM=bf16 | x3 | fp32 overrides it (A/B)."""
+        """How the window-shared conv over features runs where that GEMM is large (LV: the time-mixing features have
+        kernel_ext - 1 channels): single bf16 products with fp32 accumulation at the bf16 precision (the mode's own
+        arithmetic; LV-cfg step 76.5 -> 71.5 ms, the LV bf16 parity cases unchanged), split-bf16 products ("x3",
+        fp32-class) at the parity precisions bf16x3 / bf16x3f / bf16x2f, fp32 otherwise (None).
+        VISSM_FEATURE_GEMM=bf16 | x3 | fp32 overrides it (A/B)."""
         env = os.environ.get("VISSM_FEATURE_GEMM")
         if env:
             return None if env == "fp32" else env
-        return "x3" if (self.precision != _lib.VISSM_PREC_FP32 and self.mdef.family == "lv") else None
+        if self.precision == _lib.VISSM_PREC_FP32 or self.mdef.family != "lv":
+            return None
+        return "bf16" if self.precision == _lib.VISSM_PREC_BF16 else "x3"
 
     def flow_precisions(self):
         """(forward, backward) flow-kernel precisions of the engine's mode (host modes _lib.HOST_MODES:
