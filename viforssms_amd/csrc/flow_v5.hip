@@ -33,8 +33,12 @@
 // Supported (flow5_supports): H <= 50, k <= 64; bf16 with one hidden layer (AR) or three hidden layers with
 // the BN affine folded into the weights (LV / SV / FHN heads: bwd_kernel<3, ...>, one wave per SIMD -- its
 // three dW accumulator sets take 192 of the 512 registers), bf16x3 / bf16x2 with one hidden layer and k <= 32.
-// The AR configurations' backward (bf16, one hidden layer, k <= 8, stride 1, one window) runs bwd2_kernel:
-// two samples per unit, see below.  Everything else runs on flow_v4 / flow_v2 (exact fp32).
+// The AR configurations' backward (bf16, one hidden layer, k <= 8, stride 1, one window) runs bwd2_kernel and the
+// three-hidden-layer one-window shapes (LV / FHN / SV) bwd2n_kernel: two samples per unit, see below.  The forward of
+// every one-window shape with k <= 64 (one hidden layer at bf16 / bf16x2 with k <= 32, three hidden layers at bf16)
+// runs fwd2_kernel.  The AR kernels take the theta term folded into their layer-0 product when the caller passes the
+// theta branch's factors (VissmFlowParams.theta_rank); the fused last AR flow also runs at bf16x2 (split-weight
+// recompute).  Everything else runs on flow_v4 / flow_v2 (exact fp32).
 #include "common.hpp"
 
 // flow_v5n.hip compiles this file a second time, without the SLP vectorizer, under its own namespace and entry
