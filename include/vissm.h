@@ -130,6 +130,13 @@ typedef struct {        /* outputs of the backward: written, not accumulated */
  * win is [B] int32 window index per sample (NULL = all 0). */
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward);
 
+/* The launch geometry the flow kernels pick for d (host-side arithmetic, no GPU call): out[0] = head
+ * positions per tile, out[1] = tiles per t-chunk of a work item, out[2] = t-chunks, out[3] = sample
+ * groups.  which: 0 vissm_flow_fwd, 1 vissm_flow_bwd, 2 vissm_flow_ar_elbo_fused.  No reference
+ * equivalent (TF1 has no launch geometry): the parity tests read it at a benchmark batch and pass
+ * out[1] as chunk_tiles at a small one. */
+int vissm_flow_geometry(const VissmFlowDesc* d, int32_t which, int32_t* out);
+
 int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w,
                    const float* u, const float* C, const int32_t* win,
                    const float* theta_term, float* u_next, float* logsig,

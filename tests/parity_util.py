@@ -116,6 +116,27 @@ def build_model(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_lay
     return model
 
 
+FAMILY_SHAPE = {  # D (state dimension), n_hidden, BN, stride-2 interleaved head
+    "ar": (1, 1, False, False), "sv": (1, 3, True, False), "lv": (2, 3, True, True), "fhn": (2, 3, True, True)}
+
+
+def bench_geometry(family: str, precision: int, B: int, M: int, k: int, n_flows: int, H: int = 50) -> list:
+    """The backward launch geometry (vissm_flow_geometry, which = 1) of every flow of a `family` model at
+    batch B and window length M: what the benchmark's launch runs, for the parity cases that force it at a
+    small batch through VissmFlowDesc.chunk_tiles.  Host modes (bf16x3f / bf16x2f) run their backward at
+    bf16.  No GPU needed."""
+    from viforssms_amd import _lib
+    D, nh, bn, s2 = FAMILY_SHAPE[family]
+    prec = _lib.HOST_MODES[precision][1] if precision in _lib.HOST_MODES else precision
+    L = n_flows * k + D * M + D
+    out = []
+    for i in range(n_flows):
+        d = _lib.FlowDesc(B, L, k, H, nh, int(bn), int(s2), int(D == 2 and i < n_flows - 1), D * M, 1, prec, 0)
+        out.append(_lib.flow_geometry(d, 1))
+        L -= k
+    return out
+
+
 def oracle_inputs(model, starts):
     """time_feats [B, kext, C] and the model-specific feeds for window starts `starts`, assembled by
     the oracle's own restatement of the reference's host code from the raw series (independent of

@@ -101,6 +101,47 @@ def test_ar_cfg_bench_geometry(prec):
     _check(res, **TOL[prec])
 
 
+# The three-hidden-layer families at their benchmark launch geometry (bench.py MODEL_DEFAULTS: per-GPU B of
+# configs[2-4]).  At B = 3 / 20 the automatic geometry gives one or two sample groups and so one tile per t-chunk
+# on the bf16 kernels (LV: 314 chunks of one tile): the cross-tile transposed-conv carry of bwd2n_kernel and the
+# d theta / dW accumulation over the tiles of one item never run.  The bench launch runs chunks of ~40 (LV,
+# B = 16384), ~8 (FHN, B = 8192) and ~14 (SV, B = 16384) tiles; chunk_tiles forces the same chunks here.
+# (family, parity B, M, k, n_flows, feat_window, bench B)
+FAMILY_BENCH = {"lv": (3, 5000, 20, 3, 10, 16384), "fhn": (20, 2000, 20, 3, 10, 8192),
+                "sv": (20, 1508, 50, 5, 5, 16384)}
+# tiles per t-chunk of the first flow's backward at the bench B (vissm_flow_geometry; tests/test_lib.py pins them)
+FAMILY_BENCH_TILES = {("lv", "bf16"): 40, ("fhn", "bf16"): 8, ("sv", "bf16"): 14,
+                      ("lv", "fp32"): 79, ("fhn", "fp32"): 16, ("sv", "fp32"): 27}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("family", ["lv", "fhn", "sv"])
+def test_family_cfg_bench_geometry(family, prec):
+    """LV / FHN / SV at their config lengths with the chunk geometry of their benchmark launch: the LV / FHN / SV
+    flows (lotka_volterra_partial.py:68-104, fitz_nag_NVP.py:90-105, SV_dense.py:74-85) through the two-sample
+    three-hidden-layer backward (bf16) and the fp32 kernels with each item walking the bench's chunk of tiles."""
+    from tests.parity_util import bench_geometry
+    Bp, M, k, nf, fw, Bb = FAMILY_BENCH[family]
+    geo = bench_geometry(family, PREC[prec], Bb, M, k, nf)
+    ct = geo[0]["chunk_tiles"]
+    assert ct == FAMILY_BENCH_TILES[(family, prec)], geo
+    small = bench_geometry(family, PREC[prec], Bp, M, k, nf)
+    assert small[0]["chunk_tiles"] < ct   # the automatic geometry at the parity batch would not reach the bench's
+    res = run_parity_case(family, Bp, M, k, nf, 50, 5, fw, device=DEV, precision=PREC[prec], condition=True,
+                          chunk_tiles=ct)
+    _check(res, **TOL[prec])
+
+
+def test_lv_cfg_bench_geometry_bf16x2f():
+    """LV at the bench geometry in the parity precision bf16x2f (split-weight forward; its backward runs the bf16
+    two-sample kernel with the bench's 40-tile chunks)."""
+    from tests.parity_util import bench_geometry
+    ct = bench_geometry("lv", PREC["bf16x2f"], 16384, 5000, 20, 3)[0]["chunk_tiles"]
+    res = run_parity_case("lv", 3, 5000, 20, 3, 50, 5, 10, device=DEV, precision=PREC["bf16x2f"], condition=True,
+                          chunk_tiles=ct)
+    _check(res, **TOL["bf16x2f"])
+
+
 def test_ar_cfg_raw_draw():
     """AR-cfg with the unconditioned random draw (ELBO ~ -1e8..-1e10): the fp32 kernels' per-sample ELBO
     error stays within 4x (+1e-6) of what the same oracle executed in float32 (TF1's arithmetic) makes."""

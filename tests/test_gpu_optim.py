@@ -68,3 +68,29 @@ def test_facade_consecutive_views_update_in_place():
     assert o2._group_for(copies).flat_view is None
     for v, c in zip(views, copies):
         assert torch.equal(v, c)
+
+
+def test_facade_slots_follow_changing_groupings():
+    """var lists [a, b] -> [a] (b's gradient None) -> [a, b] again: the cached group of the first call must pick up
+    a's slots from the second call (one slot pair per variable, optimisers/adamax.py:36-40) and get_slot must keep
+    returning the live values; checked against a per-variable oracle Adamax."""
+    from optimisers.adamax import AdamaxOptimizer
+    g = torch.Generator().manual_seed(5)
+    a0, b0 = torch.randn(13, generator=g), torch.randn(7, generator=g)
+    a, b = a0.to(DEV), b0.to(DEV)
+    opt = AdamaxOptimizer(learning_rate=1e-2, beta1=0.9)
+    seq = [("ab", torch.randn(13, generator=g), torch.randn(7, generator=g)),
+           ("a", torch.randn(13, generator=g), None),
+           ("ab", torch.randn(13, generator=g), torch.randn(7, generator=g)),
+           ("a", torch.randn(13, generator=g), None),
+           ("ab", torch.randn(13, generator=g), torch.randn(7, generator=g))]
+    for _, ga, gb in seq:
+        opt.apply_gradients([(ga.to(DEV), a), (None if gb is None else gb.to(DEV), b)])
+    torch.cuda.synchronize()
+    ra, sa = _oracle_steps([a0], [[ga] for _, ga, _ in seq], 1e-2, 0.9, 0.999, 0.0, [1e-8])
+    rb, sb = _oracle_steps([b0], [[gb] for _, _, gb in seq if gb is not None], 1e-2, 0.9, 0.999, 0.0, [1e-8])
+    assert torch.allclose(a.double().cpu(), ra[0], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(b.double().cpu(), rb[0], rtol=1e-5, atol=1e-6)
+    for var, slots in ((a, sa[0]), (b, sb[0])):
+        assert torch.allclose(opt.get_slot(var, "v").double().cpu(), slots[0], rtol=1e-5, atol=1e-6)
+        assert torch.allclose(opt.get_slot(var, "m").double().cpu(), slots[1], rtol=1e-5, atol=1e-6)

@@ -63,6 +63,35 @@ def test_bf16x2_is_forward_only_without_gpu():
     assert set(_lib.HOST_MODES) <= set(_lib.TRAIN_PRECISIONS.values())
 
 
+@pytest.mark.parametrize("family,B,M,k,nf,prec,want", [
+    # the benchmark launches (bench.py MODEL_DEFAULTS, BASELINE configs[1-4]): tiles per t-chunk of flow 0's backward
+    ("ar", 65536, 5000, 8, 3, "bf16", 157),
+    ("lv", 16384, 5000, 20, 3, "bf16", 40), ("fhn", 8192, 2000, 20, 3, "bf16", 8), ("sv", 16384, 1508, 50, 5, "bf16", 14),
+    ("lv", 16384, 5000, 20, 3, "fp32", 79), ("fhn", 8192, 2000, 20, 3, "fp32", 16), ("sv", 16384, 1508, 50, 5, "fp32", 27),
+    # the parity batches without chunk_tiles: LV / FHN one tile per chunk on the bf16 kernels, SV 5
+    ("lv", 3, 5000, 20, 3, "bf16", 1), ("fhn", 20, 2000, 20, 3, "bf16", 1), ("sv", 20, 1508, 50, 5, "bf16", 5)])
+def test_flow_geometry_without_gpu(family, B, M, k, nf, prec, want):
+    """vissm_flow_geometry (host arithmetic) gives the chunk geometry the parity tests force through chunk_tiles
+    (tests/test_gpu_config_parity.py: the benchmark's launch geometry at a small batch)."""
+    from tests.parity_util import bench_geometry
+    from viforssms_amd import _lib
+    geo = bench_geometry(family, _lib.TRAIN_PRECISIONS[prec], B, M, k, nf)
+    assert geo[0]["chunk_tiles"] == want, geo
+    assert geo[0]["tile"] == (16 if prec != "fp32" else 32)
+    for g in geo:
+        assert g["n_groups"] == (B + 15) // 16 and g["n_chunks"] >= 1
+
+
+def test_flow_geometry_forced_chunk_tiles():
+    from viforssms_amd import _lib
+    d = _lib.FlowDesc(3, 10062, 20, 50, 3, 1, 1, 1, 10000, 1, _lib.VISSM_PREC_BF16, 40)
+    g = _lib.flow_geometry(d, 1)
+    assert g == {"tile": 16, "chunk_tiles": 40, "n_chunks": 8, "n_groups": 1}
+    d.k = 99
+    with pytest.raises(_lib.VissmError):
+        _lib.flow_geometry(d, 1)
+
+
 def _host():
     lib = ctypes.CDLL(HOSTCHECK)
     f = lib.vissm_host_trans
@@ -142,6 +171,25 @@ def test_softplus_ildj_matches_oracle():
         (gr,) = torch.autograd.grad(ref, [yt])
         assert abs(v - ref.item()) <= 1e-5 * max(1, abs(ref.item()))
         assert abs(g.value - gr.item()) <= 1e-4 * max(1, abs(gr.item()))
+
+
+def test_hostcheck_sanitized():
+    """The host build of elbo_math.hpp (hostcheck.cpp) under -fsanitize=address,undefined (SURVEY.md §5 race /
+    memory checking on host code; GPU sanitizers are unavailable on the pool): every model's transition gradient
+    against central finite differences over 200 states each, the softplus ILDJ, the observation term and the ABI
+    layout query, with any sanitizer report fatal."""
+    import subprocess
+    csrc = os.path.join(ROOT, "viforssms_amd", "csrc")
+    subprocess.run(["make", "-C", csrc, "build/hostcheck_san"], check=True, capture_output=True)
+    # verify_asan_link_order=0: the environment may preload a library ahead of the ASan runtime
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([os.path.join(csrc, "build", "hostcheck_san")], capture_output=True, text=True, env=env,
+                       timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
 
 
 def test_abi_struct_layouts_match_ctypes():

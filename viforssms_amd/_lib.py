@@ -81,6 +81,7 @@ SIGNATURES = {
     "vissm_normal_base_dev": (_i32, [_u64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_base_logprob": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_flow_workspace_size": (_size_t, [ctypes.POINTER(FlowDesc), _i32]),
+    "vissm_flow_geometry": (_i32, [ctypes.POINTER(FlowDesc), _i32, ctypes.POINTER(_i32)]),
     "vissm_flow_fwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size_t, _c_void_p]),
     "vissm_flow_bwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
@@ -151,6 +152,14 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = load().vissm_last_error()
         raise VissmError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def flow_geometry(desc: FlowDesc, which: int) -> dict:
+    """vissm_flow_geometry: the launch geometry the kernels pick for `desc` (which: 0 forward, 1 backward,
+    2 the fused last AR flow).  Host arithmetic only, callable without a GPU."""
+    out = (_i32 * 4)()
+    check(load().vissm_flow_geometry(ctypes.byref(desc), which, out), "vissm_flow_geometry")
+    return {"tile": out[0], "chunk_tiles": out[1], "n_chunks": out[2], "n_groups": out[3]}
 
 
 def ptr(t) -> Optional[int]:

@@ -10,6 +10,10 @@ namespace vissm {
 
 size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
 size_t flow4_workspace_size(const VissmFlowDesc* d, int backward);
+void flow2_geometry(const VissmFlowDesc* d, int backward, int32_t* out);
+void flow4_geometry(const VissmFlowDesc* d, int backward, int32_t* out);
+void flow5_geometry(const VissmFlowDesc* d, int which, int32_t* out);
+void flow5_geometry_nh3(const VissmFlowDesc* d, int which, int32_t* out);
 int flow4_fwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
               float*, float*, void*, size_t, hipStream_t);
 int flow4_bwd(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*, const float*,
@@ -82,6 +86,21 @@ size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
   if (use_v5(d)) return use_nh3(d) ? flow5_workspace_size_nh3(d, backward) : flow5_workspace_size(d, backward);
   return use_flow4(d) ? flow4_workspace_size(d, backward) : flow2_workspace_size(d, backward);
+}
+
+int vissm_flow_geometry(const VissmFlowDesc* d, int32_t which, int32_t* out) {
+  int rc = validate(d);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(out && which >= 0 && which <= 2, "flow_geometry: bad which=%d or null out", which);
+  if (which == 2) {
+    VISSM_CHECK_ARG(flow5_ar_fused_supports(d), "flow_geometry: the descriptor has no fused AR(1) last flow");
+    flow5_geometry(d, 2, out);
+  } else if (use_v5(d)) {
+    (use_nh3(d) ? flow5_geometry_nh3 : flow5_geometry)(d, which, out);
+  } else {
+    (use_flow4(d) ? flow4_geometry : flow2_geometry)(d, which, out);
+  }
+  return VISSM_OK;
 }
 
 int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,

@@ -849,6 +849,12 @@ size_t flow4_workspace_size(const VissmFlowDesc* d, int backward) {
   return backward ? bwd_ws_layout(d, g, nullptr, nullptr) : fwd_ws_layout(d, g, nullptr, nullptr);
 }
 
+void flow4_geometry(const VissmFlowDesc* d, int backward, int32_t* out) {
+  using namespace flow4;
+  Geom g = geom(d, backward != 0);
+  out[0] = P; out[1] = g.CH / P; out[2] = g.n_chunks; out[3] = g.n_groups;
+}
+
 int flow4_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
               const float* theta_term, float* u_next, float* logsig, void* workspace, size_t ws_bytes,
               hipStream_t st) {

@@ -3082,6 +3082,13 @@ size_t VISSM_FLOW5_API(flow5_workspace_size)(const VissmFlowDesc* d, int backwar
   return ws_layout(d, g, backward != 0, nullptr, nullptr);
 }
 
+// which: 0 forward, 1 backward, 2 the fused last AR flow (15 outputs per 16-column tile)
+void VISSM_FLOW5_API(flow5_geometry)(const VissmFlowDesc* d, int which, int32_t* out) {
+  const int po = which == 2 ? P - 1 : P;
+  Geom g = geom(d, which != 0, po);
+  out[0] = po; out[1] = g.CH / po; out[2] = g.n_chunks; out[3] = g.n_groups;
+}
+
 #define FLOW5_DISPATCH(KERNEL, NHd, JB, NP, ...)                                                  \
   do {                                                                                             \
     if (NP == 3) {                                                                                 \

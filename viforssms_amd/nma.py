@@ -448,13 +448,17 @@ class Engine:
         """How the window-shared conv over features runs where that GEMM is large (LV: the time-mixing features have
         kernel_ext - 1 channels): single bf16 products with fp32 accumulation at the bf16 precision (the mode's own
         arithmetic; LV-cfg step 76.5 -> 71.5 ms, the LV bf16 parity cases unchanged), split-bf16 products ("x3",
-        fp32-class) at the parity precisions bf16x3 / bf16x3f / bf16x2f, fp32 otherwise (None).
-        VISSM_FEATURE_GEMM=bf16 | x3 | fp32 overrides it (A/B)."""
-        env = os.environ.get("VISSM_FEATURE_GEMM")
-        if env:
-            return None if env == "fp32" else env
+        fp32-class) at the parity precisions bf16x3 / bf16x3f / bf16x2f, fp32 otherwise (None).  For LV at a
+        non-fp32 precision only, Engine.feature_gemm_override or VISSM_FEATURE_GEMM = bf16 | x3 | fp32 replaces the
+        choice (A/B timing; tests that isolate the flow kernels from the bf16 rounding of these GEMMs); fp32 runs
+        and the other families never change arithmetic."""
         if self.precision == _lib.VISSM_PREC_FP32 or self.mdef.family != "lv":
             return None
+        mode = getattr(self, "feature_gemm_override", None) or os.environ.get("VISSM_FEATURE_GEMM")
+        if mode:
+            if mode not in ("bf16", "x3", "fp32"):
+                raise ValueError(f"feature GEMM mode {mode!r} is not bf16 / x3 / fp32")
+            return None if mode == "fp32" else mode
         return "bf16" if self.precision == _lib.VISSM_PREC_BF16 else "x3"
 
     def flow_precisions(self):

@@ -72,20 +72,24 @@ class AdamaxOptimizer:
     # -- slots --------------------------------------------------------------------------
     def _group_for(self, vars_: List[torch.Tensor]) -> _Group:
         """The flat-slot group of exactly these variables.  A variable first seen in another grouping (a None
-        gradient on one call, a changed var_list) keeps its Adamax state: its current slot values are copied
-        into the new group's flat buffers, as TF keeps one slot pair per variable (optimisers/adamax.py:36-40).
-        Groups hold their variables, so the ids in a key cannot be reused while the group exists."""
+        gradient on one call, a changed var_list) keeps its Adamax state, as TF keeps one slot pair per variable
+        (optimisers/adamax.py:36-40): _slot_of[id(var)] is the single record of where a variable's live slots
+        are, and whenever it points outside the group about to run (a new group, or a cached one another
+        grouping has run since), the current values are copied into the group's flat buffers and the record
+        repointed.  Groups hold their variables, so the ids in a key cannot be reused while the group exists."""
         key = tuple(id(v) for v in vars_)
         g = self._groups.get(key)
         if g is None or any(a is not b for a, b in zip(g.vars, vars_)):
             g = self._groups[key] = _Group(vars_)
-            with torch.no_grad():
-                for var, sv, sm in zip(vars_, g.slot_views("v"), g.slot_views("m")):
-                    old = self._slot_of.get(id(var))
-                    if old is not None and old["var"] is var:
-                        sv.copy_(old["v"])
-                        sm.copy_(old["m"])
-                    self._slot_of[id(var)] = {"var": var, "v": sv, "m": sm}
+        with torch.no_grad():
+            for var, sv, sm in zip(vars_, g.slot_views("v"), g.slot_views("m")):
+                old = self._slot_of.get(id(var))
+                if old is not None and old["var"] is var and old["v"].data_ptr() == sv.data_ptr():
+                    continue   # the group's own views are the live slots
+                if old is not None and old["var"] is var:
+                    sv.copy_(old["v"])
+                    sm.copy_(old["m"])
+                self._slot_of[id(var)] = {"var": var, "v": sv, "m": sm}
         return g
 
     def get_slot(self, var, name):
