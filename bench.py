@@ -12,11 +12,13 @@ launch (2 x F_fwd per sample and head position, SURVEY.md §8d -- the recomputed
 counted) divided by its average launch time, measured live with HIP events on the launch stream
 during the timed steps; mixed_roof_frac prices the same FLOPs with the vector terms at the fp32
 vector peak.  step_roofline: sum of every kernel's t_min under its own roof / measured step time.
-parity_precision: the same step timed with bf16x3 flow products (ELBO within 1e-4 of the oracle).
+parity_precision: the same step timed at the precisions that hold the per-sample ELBO within 1e-4 of the
+oracle -- bf16x2f (split-weight forward), bf16x3f and bf16x3 (every product split; gradient within 1e-3 too).
 cpu_baseline: the fp32 CPU restatement of the same step (oracle/, "port") on a bounded sample of
 trajectories, timed on this host, plus the AR plumbing config (p = 50, M = 50, k = 50) at true size.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]  (N > 1 under torch.distributed.run)
+Usage: python bench.py [--gpus N --steps K --warmup W]  (N > 1: launched by torch.distributed.run with
+--gpus N, or started as plain `python bench.py --gpus N`, which spawns the N ranks itself)
 """
 from __future__ import annotations
 
@@ -130,13 +132,41 @@ def host_cpu():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), or None when unlimited / unreadable: on a
+    shared GPU box `nproc` lists the whole machine while the job's share is smaller."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, obs, ob, tt):
-    """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories."""
+    """fp32 CPU restatement (oracle/) of the same step on a bounded sample of trajectories, timed at the
+    process's default thread count (OMP_NUM_THREADS: the box's CPU share) and at `nproc` threads
+    (len(sched_getaffinity)); `value` / `cores` are the faster of the two."""
+    import torch
     B = min(args.cpu_B, args.B)
-    t, n, cores = _cpu_ar_step_rate(B, args.M, args.k, args.T, obs, ob, tt, args.cpu_seconds, args.cpu_min_steps)
-    return {"value": B * args.M / t, "unit": "transitions/s", "cores": cores, "kind": "port", "host": host_cpu(),
+    host = host_cpu()
+    default_threads = torch.get_num_threads()
+    lines = []
+    for threads in sorted({default_threads, host["nproc"]}):
+        torch.set_num_threads(threads)
+        secs = args.cpu_seconds if threads == default_threads else args.cpu_seconds / 2
+        t, n, _ = _cpu_ar_step_rate(B, args.M, args.k, args.T, obs, ob, tt, secs, args.cpu_min_steps)
+        lines.append({"threads": threads, "value": B * args.M / t, "s_per_step": t, "steps": n})
+    torch.set_num_threads(default_threads)
+    best = max(lines, key=lambda x: x["value"])
+    host["cgroup_cpus"] = cgroup_cpus()
+    return {"value": best["value"], "unit": "transitions/s", "cores": best["threads"], "kind": "port", "host": host,
+            "by_threads": lines,
             "sample": f"fp32 CPU restatement of the TF1 step (oracle/nma_oracle.py) on B={B} trajectories x "
-                      f"M={args.M} (T={args.T}, k={args.k}), median of {n} steps after 2 warm-up ({t:.2f} s/step)"}
+                      f"M={args.M} (T={args.T}, k={args.k}), median of the steps after 2 warm-up, at "
+                      f"{' and '.join(str(x['threads']) for x in lines)} torch threads (nproc = {host['nproc']}, "
+                      f"cgroup CPU quota = {host['cgroup_cpus']}); value = the faster ({best['threads']} threads, "
+                      f"{best['s_per_step']:.2f} s/step)"}
 
 
 def cpu_baseline_ar_plumbing(args):
@@ -483,7 +513,13 @@ def main():
     args = parse_args()
 
     import torch
-    from viforssms_amd.launch import init_distributed
+    from viforssms_amd.launch import ensure_world, init_distributed
+
+    # --gpus N without torchrun: launch N ranks (torchrun, 127.0.0.1) from here before any GPU call and exit with
+    # their status; under torchrun the world must be N
+    rc = ensure_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
 
     ctx = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -4,8 +4,10 @@ Same file format, flags and order of numpy-RNG draws as the reference main.py: t
 when the data generator and the model modules are imported (AR_dat_gen.py:3, AR.py:18), then
 data_gen writes dat/AR_*.txt, AR.main draws the q(theta) permutations and the training loop
 draws the windows.  The ELBO step itself runs on the GPU (libvissm HIP kernels).
-Multi-GPU: ``torchrun --nproc-per-node N main.py hyperparameters.txt -p P`` shards the p samples.
+Multi-GPU: ``torchrun --nproc-per-node N main.py hyperparameters.txt -p P`` (or ``python main.py
+hyperparameters.txt -p P --gpus N``, which launches the N ranks itself) shards the p samples.
 """
+import os
 import sys
 
 import numpy as np
@@ -29,10 +31,15 @@ def run(argv=None):
         sys.exit("Please specify a valid hyperparameter file")
     hp = apply_overrides(hp, args)
 
+    from viforssms_amd.launch import barrier, ensure_world, init_distributed
+    if args.gpus is not None:
+        rc = ensure_world(args.gpus, os.path.abspath(__file__), sys.argv[1:] if argv is None else list(argv))
+        if rc is not None:
+            sys.exit(rc)
+
     from viforssms_amd import ar
     from viforssms_amd._lib import TRAIN_PRECISIONS
     from viforssms_amd.data import data_gen
-    from viforssms_amd.launch import barrier, init_distributed
 
     ctx = init_distributed()
     data_gen(hp.T, hp.impute, hp.x0, np.array(hp.theta), hp.obs_std, write=(ctx.rank == 0))

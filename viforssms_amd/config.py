@@ -115,6 +115,9 @@ def handle_opts(argv=None):
     # additions of this build
     parser.add_argument("-p", "-samples", action="store", dest="p", default=None,
                         help="Samples (windows) per step; overrides the file's p")
+    parser.add_argument("--gpus", type=int, default=None,
+                        help="Ranks (one per GPU): without torchrun, N > 1 launches N ranks itself; under torchrun "
+                             "the launched world must equal N.  Default: the launcher's world (1 without one)")
     parser.add_argument("--steps", type=int, default=None, help="Stop after this many runs (default: endless)")
     parser.add_argument("--seed", type=int, default=1, help="Philox seed of the base noise")
     parser.add_argument("--precision", choices=["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x2f"], default="fp32",

@@ -3318,6 +3318,9 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
   const bool x2 = d->precision == VISSM_PREC_BF16X2;
+  // bf16x2 has only the two-sample kernel: it must meet that kernel's geometry (bwd2_ok minus the precision test)
+  VISSM_CHECK_ARG(!x2 || (g.S == S && !g.dcb && d->n_win == 1 && d->k <= KP2),
+                  "flow_ar_elbo_fused: bf16x2 needs the two-sample kernel's geometry (one window, k <= %d)", KP2);
   const bool b2 = x2 || bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
   launch_prep(d, w, ws, fold, st);
   launch_pad(d, w, g, C, theta_term, ws, fold, st);

@@ -3,10 +3,49 @@ RCCL ("nccl" backend on ROCm) when launched by torchrun, gloo on CPU-only hosts.
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
+from typing import List, Optional
 
 import torch
 
 from .vi_ssm import DistCtx
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(gpus: int, script: str, argv: List[str], port: Optional[int] = None) -> List[str]:
+    """The torchrun command that runs `script argv` as `gpus` ranks on this node (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port or _free_port()), script] + list(argv)
+
+
+def ensure_world(gpus: int, script: str, argv: List[str]) -> Optional[int]:
+    """`--gpus N` of bench.py / main.py.  Under torchrun (WORLD_SIZE set) the launched world must be N: a mismatch
+    exits non-zero.  Without WORLD_SIZE and N > 1 this process becomes a launcher: it starts N rank processes
+    with torchrun BEFORE any GPU call (no torch.cuda use here: a process that initialised the GPU must not be
+    replaced, and its children get the devices) and returns their exit code for the caller to exit with.
+    Returns None when this process is itself the (only) rank and should run the work."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {gpus})")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != gpus:
+            raise SystemExit(f"--gpus {gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+        return None
+    if gpus == 1:
+        return None
+    n_dev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    backend = os.environ.get("VISSM_DIST_BACKEND", "nccl")
+    if 0 < n_dev < gpus and backend != "gloo":
+        raise SystemExit(f"--gpus {gpus} needs {gpus} visible GPUs for RCCL, found {n_dev} "
+                         "(VISSM_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
+    return subprocess.call(rank_launch_cmd(gpus, script, argv))
 
 
 def init_distributed() -> DistCtx:

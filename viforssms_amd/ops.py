@@ -188,15 +188,20 @@ class MAFlowFn(torch.autograd.Function):
                                  ptr(u_next), ptr(logsig), ptr(ws), wsz, _lib.stream_handle(dev)),
               "vissm_flow_fwd")
         ctx.shape = shape
-        ctx.tf = tf  # constants (no gradient flows through them: theta_term carries it)
-        ctx.save_for_backward(win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)
+        # the theta-fold factors are constants here (theta_term carries their gradient) but are saved like the
+        # rest, so autograd's version check catches an in-place change between forward and backward
+        tf = tuple(tf) if tf is not None else ()
+        ctx.n_tf = len(tf)
+        ctx.save_for_backward(win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, *tf)
         return u_next, logsig
 
     @staticmethod
     def backward(ctx, g_next, g_ls):
         lib = _lib.load()
         shape: FlowShape = ctx.shape
-        win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head = saved[:11]
+        tf = tuple(saved[11:]) if ctx.n_tf else None
         dev = u.device
         if g_next is None:
             g_next = torch.zeros(shape.B, shape.Lout, dtype=torch.float32, device=dev)
@@ -216,7 +221,7 @@ class MAFlowFn(torch.autograd.Function):
         grads = FlowGrads(*[ptr(t) for t in gw])
         wsz = lib.vissm_flow_workspace_size(ctypes.byref(d), 1)
         ws = _workspace(wsz, dev)
-        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, ctx.tf)
+        prm = _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf)
         check(lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(prm), ptr(u), ptr(C), ptr(win), ptr(theta_term),
                                  ptr(g_next), ptr(g_ls), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws),
                                  wsz, _lib.stream_handle(dev)), "vissm_flow_bwd")
