@@ -428,6 +428,9 @@ def measure(args, ctx, dev, parity_line: bool):
         "data": meta["data"],
         "config": {"workload": meta["workload"], "global_batch": B * world, "seq_len": args.T,
                    "parallelism": f"dp{world}", "hip_graph": bool(args.graph),
+                   # gradient bytes SUM-all-reduced per step and rank (LV at >1 ranks: each flow's dC instead of
+                   # its window-shared variables, vi_ssm.VISSMBase._shared_grad_plan)
+                   "allreduce_bytes_per_step": int(getattr(model, "last_allreduce_bytes", 0)),
                    "last_flow_fused": bool(model.engine.fused_ok(model.batch_for(model.select_windows()), B))},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,

@@ -40,7 +40,7 @@ def _model(family="ar"):
     return build_model(family, B, M, k, nf, H, nl, fw, "cuda:0", T=T, precision=prec, seed=3)
 
 
-def _worker(rank, world, port, overlap, family, out):
+def _worker(rank, world, port, overlap, family, out, shared=True):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -50,21 +50,22 @@ def _worker(rank, world, port, overlap, family, out):
     model.dist = DistCtx(rank, world)
     model.p_local = P // world
     model.overlap_allreduce = overlap
+    model.shared_dc_allreduce = shared
     np.random.seed(SEED)
     starts = model.select_windows()
     o = model.elbo_step(model.batch_for(starts), 0)
     torch.cuda.synchronize()
     out.put((rank, overlap, starts, model.store.grad.cpu().numpy(), model.store.flat.cpu().numpy(),
-             o["elbo"].cpu().numpy(), float(o["global_norm"][0])))
+             o["elbo"].cpu().numpy(), float(o["global_norm"][0]), model.last_allreduce_bytes))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(overlap, family):
+def _run(overlap, family, shared=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, overlap, family, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, overlap, family, q, shared)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -97,7 +98,7 @@ def test_two_rank_hip_gradient_equals_full_batch_and_params_agree(family):
     full_p = model.store.flat.double().cpu().numpy()
     full_e = o["elbo"].cpu().numpy()
     for res in (ov, blk):
-        (_, _, s0, g0, p0, e0, n0), (_, _, s1, g1, p1, e1, n1) = res[0], res[1]
+        (_, _, s0, g0, p0, e0, n0, _), (_, _, s1, g1, p1, e1, n1, _) = res[0], res[1]
         assert np.array_equal(s0, starts) and np.array_equal(s1, starts)
         # the ranks' ELBOs are the two halves of the full batch (same Philox rows)
         assert np.allclose(np.concatenate([e0, e1]), full_e, rtol=1e-5, atol=1e-5 * np.abs(full_e).max())
@@ -109,3 +110,18 @@ def test_two_rank_hip_gradient_equals_full_batch_and_params_agree(family):
         keep = np.abs(full_g) > 1e-4 * np.abs(full_g).max()
         assert np.abs(p0 - full_p)[keep].max() < 2e-6
     assert np.array_equal(ov[0][3], blk[0][3])              # bucketed + overlapped == one blocking reduce
+
+
+def test_lv_window_shared_gradients_summed_through_dC():
+    """LV, one window on both ranks: each flow's dC (and w_eps gradient) is SUM-all-reduced inside the backward and
+    the window-shared backward (feature MLP, conv over the time-mixing features: lotka_volterra_partial.py:71-82)
+    runs replicated on it, so those variables leave the gradient all-reduce (VISSMBase._shared_grad_plan).  Same
+    gradient as all-reducing every variable (linear in dC), fewer bytes, ranks bitwise equal."""
+    via_dc = _run(True, "lv", shared=True)
+    full = _run(True, "lv", shared=False)
+    g_dc, g_full = via_dc[0][3], full[0][3]
+    assert np.array_equal(via_dc[0][3], via_dc[1][3]) and np.array_equal(via_dc[0][4], via_dc[1][4])
+    assert np.linalg.norm(g_dc - g_full) / np.linalg.norm(g_full) < 1e-4
+    b_dc, b_full = via_dc[0][7], full[0][7]
+    print({"allreduce_bytes_via_dC": b_dc, "allreduce_bytes_all_variables": b_full})
+    assert 0 < b_dc < b_full

@@ -181,27 +181,15 @@ __device__ __forceinline__ float elu_fast(float x) {
 __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
 }
-#ifndef VISSM_FWD_HWLOG
-#define VISSM_FWD_HWLOG 1  // forward kernels: log sigma on v_log_f32 (sigma >= 1e-10: a normal float; AR-cfg fwd 7.56 -> 7.34 ms)
-#endif
-#ifndef VISSM_SOFTPLUS_HW
-#define VISSM_SOFTPLUS_HW 1  // softplus on v_exp_f32 / v_log_f32 directly (__logf adds a denormal-scaling
-                             // and refinement sequence; 1 + e^-|x| lies in [1, 2]) and max(x, 0) as a median
-#endif
+// (the forward kernels take log sigma on v_log_f32: sigma >= 1e-10 is a normal float; AR-cfg fwd 7.56 -> 7.34 ms)
+// softplus on v_exp_f32 / v_log_f32 directly (__logf adds a denormal-scaling and refinement sequence; 1 + e^-|x|
+// lies in [1, 2]) and max(x, 0) as a median
 __device__ __forceinline__ float softplus_fast(float x) {
-  if constexpr (VISSM_SOFTPLUS_HW)
-    return __builtin_amdgcn_fmed3f(x, 0.f, 3.0e38f) +
-           __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-kLog2e * fabsf(x))) * kLn2;
-  else
-    return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x)));
+  return __builtin_amdgcn_fmed3f(x, 0.f, 3.0e38f) +
+         __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-kLog2e * fabsf(x))) * kLn2;
 }
-#ifndef VISSM_RCP_FAST
-#define VISSM_RCP_FAST 1  // v_rcp_f32 (1 ulp) instead of the correctly rounded division sequence of __frcp_rn
-#endif
-__device__ __forceinline__ float rcp_f(float x) {
-  if constexpr (VISSM_RCP_FAST) return __builtin_amdgcn_rcpf(x);
-  else return __frcp_rn(x);
-}
+// v_rcp_f32 (1 ulp) instead of the correctly rounded division sequence of __frcp_rn (-1.1 ms per AR-cfg step)
+__device__ __forceinline__ float rcp_f(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float sigmoid_fast(float x) { return rcp_f(1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------
@@ -211,35 +199,16 @@ __device__ __forceinline__ float sigmoid_fast(float x) { return rcp_f(1.f + __ex
 //   WE(kb, ob)     16NH + kb*4 + ob         layer 0            A[h][j]
 //   WC(jb, ks)     16NH + 4KB + jb*2 + ks   dcon               A[j][h perm]
 //   WH(ks)         16NH + 4KB + 2JB + ks    head               A[o][h perm]
-//   IS(ob)         16NH + 4KB + 2JB + 2+ob  dC selection       identity (exact; hi plane only)
 // With batch_normalization(training=False) after each hidden ELU (LV / SV / FHN), the BN affine
 // x = gamma' e + beta is folded into the layer that consumes it: W~ = diag(gamma') W and
 // b~ = b + W^T beta (head likewise), so the kernels only see ELU outputs E; the BN and
 // unfolded weight gradients are recovered from the reduced sums in scatter_wgrad_kernel.
 // ---------------------------------------------------------------------------
-// head fragments replicate the two output rows into every lane group (VISSM_HEAD_REP)
-#ifndef VISSM_HEAD_REP
-#define VISSM_HEAD_REP 1
-#endif
-// (the backward sums the dC tile with VALU adds by default: no IS fragments then)
-#ifndef VISSM_BWD_VALU_DC
-#define VISSM_BWD_VALU_DC 1
-#endif
-__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) {
-  return 16 * NH + 4 * KB + 2 * JB + (VISSM_BWD_VALU_DC ? 2 : 6);
-}
-
-// phase-ablation mask for timing experiments (build with -DVISSM_V5_ABLATE=mask; results are
-// then wrong by construction).  A compile-time constant: a runtime mask splits the unit into
-// basic blocks the scheduler cannot interleave across.
-#ifndef VISSM_V5_ABLATE
-#define VISSM_V5_ABLATE 0
-#endif
-constexpr int kAbl = VISSM_V5_ABLATE;
+// (head fragments replicate the two output rows into every lane group)
+__host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * NH + 4 * KB + 2 * JB + 2; }
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
-  int dcb;  // backward: the block's waves share a chunk and sum their dC tiles (one window)
   int dc16;  // backward, bf16 products, one window: the dC slab holds bf16 partials (half the reduce's reads)
   int ncu;  // compute units of the device (the backward's wave priority pattern)
 };
@@ -274,16 +243,9 @@ __device__ __forceinline__ float row_next(float v) {  // lane c <- lane c + 1 (c
                                                                0x101, 0xf, 0xf, false));
 }
 
-// backward dC tiles summed over a block's NW groups before the slab (one window only): the dC
-// slab per AR-cfg launch 4.1 -> 1.0 GB and its reduce 0.74 -> 0.19 ms, but the tile barriers'
-// wave skew costs the kernel 0.8 ms: measured 126.9 vs 125.8 ms per AR-cfg step, so off
-#ifndef VISSM_BWD_DCB
-#define VISSM_BWD_DCB 0
-#endif
-// bf16 dC slab partials at bf16 products, one window (read by launch_reduce_rows_bf16)
-#ifndef VISSM_BWD_DC16
-#define VISSM_BWD_DC16 1
-#endif
+// bf16 dC slab partials at bf16 products, one window (read by launch_reduce_rows_bf16).  (Summing the dC tiles over
+// a block's groups through LDS before the slab -- slab 4.1 -> 1.0 GB and its reduce 0.74 -> 0.19 ms per AR-cfg
+// launch -- cost the kernel 0.8 ms in tile-barrier wave skew: 126.9 vs 125.8 ms per step, round 1; removed.)
 
 // folded hidden weight W~_l[hin][hout] and head weight W~_h[h][o]
 __device__ __forceinline__ float wt_hid(const VissmFlowParams& w, int H, int bn, int l, int hin, int hout) {
@@ -355,16 +317,14 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
       const int jb = r >> 1, ks = r & 1;
       const int jt = 16 * jb + c, h = swz(hperm(ks, g, j));
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
-    } else if ((r -= 2 * JB) < 2) {  // WH
+    } else {  // WH
+      r -= 2 * JB;
       const int h = swz(hperm(r, g, j));
-      // output rows o' = 4 q + o (o = 0: mu, 1: sigma) for every q with VISSM_HEAD_REP: each lane
-      // group receives (mu, r) of its column in registers 0, 1 of the head MFMA (no shuffle)
-      const int o = VISSM_HEAD_REP ? (c & 3) : c;
+      // output rows o' = 4 q + o (o = 0: mu, 1: sigma) for every q: each lane group receives (mu, r) of its
+      // column in registers 0, 1 of the head MFMA (no shuffle)
+      const int o = c & 3;
       if (o < 2 && h < H) x = wt_head(w, H, bn, nh, h, o) * kLn2;
       else if (o < 2 && h == HP - 1) x = bias_head(w, H, bn, nh, o);
-    } else {  // IS
-      const int ob = r - 2;
-      x = hperm(ob >> 1, g, j) == 16 * ob + c ? 1.f : 0.f;
     }
     v[j] = x;
   }
@@ -438,106 +398,32 @@ struct Shared {
 // Compiler-only fence: keeps the (loop-invariant) LDS weight-fragment loads next to their
 // use instead of hoisted out of the unit loop with ~100-200 VGPRs live.
 __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
-// the forward kernel's fences (BWD = false) are optional: with its small register footprint the
-// compiler may keep weight fragments in registers across units
-// Forward kernel: the 8 NH + 4 KB + 2 weight fragments it uses live in registers for the whole
-// item (its footprint allows it) and its fences are off; measured 11.8 -> 10.4 ms per AR-cfg
-// launch.  (The backward keeps its fences: ~250 VGPRs leave no room to hoist anything.)
-#ifndef VISSM_FWD_REGW
-#define VISSM_FWD_REGW 1
-#endif
-// bf16x2 forward (split weights): 0 both planes in registers, 1 hi planes in registers and lo planes
-// read from LDS per use, 2 both from LDS
-#ifndef VISSM_FWD_X2
-#define VISSM_FWD_X2 1
-#endif
-#ifndef VISSM_FWD_FENCE
-#define VISSM_FWD_FENCE 0
-#endif
-template <bool BWD>
-__device__ __forceinline__ void fence_fwd() {
-  if constexpr (BWD || VISSM_FWD_FENCE) fence();
-}
-// backward variants (A/B switches): ELU select as v_med3 in the recompute; dC summed with fp32
-// VALU adds instead of the identity-selection MFMA; per-position LDS writes by every lane instead
-// of a divergent branch (the lanes of a column hold identical values)
-#ifndef VISSM_BWD_MED3
-#define VISSM_BWD_MED3 0
-#endif
-#ifndef VISSM_BWD_KFIX
-#define VISSM_BWD_KFIX 8  // > 0: a straight-line transposed-conv sum when k equals it
-#endif
-#ifndef VISSM_BWD_GIMG
-#define VISSM_BWD_GIMG 1  // one hidden layer: the head gradient rides in the dZ image (no G fragment via LDS)
-#endif
-#ifndef VISSM_BWD_I0REG
-#define VISSM_BWD_I0REG 1  // one hidden layer, bf16: elu'(I_0) from registers instead of reading the image back
-#endif
-#ifndef VISSM_BWD_DTHATOM
-#define VISSM_BWD_DTHATOM 0  // the per-sample d theta sums as no-return LDS adds
-#endif
-#ifndef VISSM_BWD_BATCHW
-#define VISSM_BWD_BATCHW 30  // bits (one hidden layer), all read before the head-backward VALU
-                             // unless noted: 2 the dX weight fragments, 4 the dcon fragments (before
-                             // elu'(I_0)), 8 dW's I_0 fragments, 16 dW_eps's u fragments, 32 the
-                             // transposed conv's carry-in (measured: no further gain, off); reading
-                             // the recompute's fragments a phase ahead measured no gain
-#endif
-#ifndef VISSM_BWD_DWLATE
-#define VISSM_BWD_DWLATE 3  // one hidden layer: the dW / dW_head MFMAs (off the unit's critical path) issued
-                            // later from fragments read at their usual place: 1 after the dA0 image store,
-                            // 2 after the dW_eps / d theta products, 3 after the dcon stores of the du section,
-                            // 4 at the end of the unit.  Issued where they were (0), the 20 MFMAs sat between
-                            // dX and elu'(I_0) on the unit's dependency chain: 105.6 -> 104.3 ms per step (3;
-                            // 1: 105.1, 2: 105.5; A/B, profiles/r02/dw_late_ab.log)
-#endif
-#ifndef VISSM_FZ_ZCEARLY
-#define VISSM_FZ_ZCEARLY 1  // fused AR(1) variant: the previous tile's last x (LDS carry) read with the unit's inputs:
-                            // 104.6 -> 104.2 ms per step; the log sigma column sums' read-modify-write moved to the
-                            // unit's end as well: 106.5 (A/B, profiles/r02/fz_lds_ab.log)
-#endif
-#ifndef VISSM_BWD_DTHRMW
-#define VISSM_BWD_DTHRMW 1  // the per-sample d theta read-modify-writes branch-free, reads issued together
-#endif
-#ifndef VISSM_BWD_DUTREE
-#define VISSM_BWD_DUTREE 1  // the straight-line transposed-conv sum as reads first, then a pairwise sum
-#endif
-#ifndef VISSM_ACC_INIT
-#define VISSM_ACC_INIT 1  // layer-0 products accumulate onto C + theta
-#endif
-#ifndef VISSM_BWD_UNCOND
-#define VISSM_BWD_UNCOND 0
-#endif
-#ifndef VISSM_BWD_FENCES
-#define VISSM_BWD_FENCES 0xff
-#endif
-#ifndef VISSM_BWD_PRIO
-#define VISSM_BWD_PRIO 3
-#endif
-#ifndef VISSM_FWD_PRIO
-#define VISSM_FWD_PRIO 3  // forward: the same round-mod-4 priority (four blocks per CU): 9.45 -> 9.15 ms
-#endif
-#ifndef VISSM_LANE_SCALARS
-#define VISSM_LANE_SCALARS 1  // per-sample window index / d log q read once per item into lane b, then
-                              // v_readlane per unit (no scalar load + lgkmcnt(0) drain per unit)
-#endif
-#ifndef VISSM_BWD_WHP
-#define VISSM_BWD_WHP 1  // head-backward A fragments: all four LDS reads issued unconditionally up front
-                         // (a masked read per MFMA serialised four LDS round trips)
-#endif
+// Forward kernel: the 8 NH + 4 KB + 2 weight fragments it uses live in registers for the whole item (its
+// footprint allows it) and it has no fences; measured 11.8 -> 10.4 ms per AR-cfg launch.  The bf16x2 forward
+// (split weights) keeps the hi planes in registers and reads the lo planes from LDS per use (both planes in
+// registers 12.5, both from LDS 12.9 ms against 11.6).  The backward keeps its fences between phases: at ~250
+// VGPRs nothing may be hoisted.
+//
+// Backward design decisions (A/B measurements): one hidden layer -- the head gradient rides in
+// the dZ image (no G fragment via LDS), elu'(I_0) from the bf16 pairs the recompute keeps in registers, the dX and
+// dcon weight fragments, dW's I_0 and dW_eps's u fragments all read before the head-backward VALU block; the dW /
+// dW_head MFMAs (off the unit's critical path) issued after the du section's dcon stores (105.6 -> 104.3 ms per
+// step; after the dA0 image store 105.1, after the dW_eps / d theta products 105.5, profiles/r02/dw_late_ab.log);
+// the fused AR(1) variant reads the previous tile's last x (LDS carry) with the unit's inputs (104.6 -> 104.2);
+// the per-sample d theta read-modify-writes branch-free with their reads issued together (no-return LDS adds: no
+// change); k = 8: a straight-line transposed-conv sum, reads first, then a pairwise tree; per-sample window index /
+// d log q read once per item into lane b, then v_readlane per unit; the four head-backward A fragments read
+// unconditionally up front (a masked read per MFMA serialised four LDS round trips).  Rejected: the ELU select as
+// v_med3 in the one-sample recompute (30.4 vs 29.7 ms), per-position LDS writes by every lane instead of a branch.
 // value of lane `bl` of v (bl wave-uniform)
 __device__ __forceinline__ int lane_i(int v, int bl) { return __builtin_amdgcn_readlane(v, bl); }
 __device__ __forceinline__ float lane_f(float v, int bl) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), bl));
 }
-template <int BIT>
-__device__ __forceinline__ void fence_bwd() {
-  if constexpr ((VISSM_BWD_FENCES >> BIT) & 1) fence();
-}
-template <bool BWD, int BIT>
+// unit_forward's fences: in the backward's recompute only
+template <bool BWD>
 __device__ __forceinline__ void fence_uf() {
-  if constexpr (BWD) fence_bwd<BIT>();
-  else fence_fwd<false>();
+  if constexpr (BWD) fence();
 }
 
 template <int NH, int KB, int JB, int NP>
@@ -564,14 +450,11 @@ __device__ __forceinline__ void load_shared(Shared<NH, KB, JB, NP>& sh, const bf
 // slot bit 0 and so in row parity, i.e. in the 128-B half of the bank row), and the transposed read
 // (ds_read_b64_tr_b16, 32-lane halves = rows 8h .. 8h + 7 x chunks 4hb .. 4hb + 3: the four rows of
 // one parity take four different 4-slot blocks through slot bits 2-3 = (p2, p3 ^ p1)).  The plain
-// `ch ^ p` layout (VISSM_TIMG_SWZ=0) gave the transposed reads 2-way conflicts (rows p and p ^ 2
-// shared slot blocks): SQ_LDS_BANK_CONFLICT per bf16 backward launch 2.16e8 -> 4.1e7 cycles, step
-// 118.5 -> 117.5 ms (A/B, profiles/r02/lds_swizzle_ab.log).  A full bit permutation of p that is
-// equally conflict-free cost 26 more instructions and a spill: 121.6 ms.
-#ifndef VISSM_TIMG_SWZ
-#define VISSM_TIMG_SWZ 1
-#endif
-__host__ __device__ constexpr int timg_perm(int p) { return VISSM_TIMG_SWZ ? (p ^ ((p & 2) << 2)) : p; }
+// `ch ^ p` layout gave the transposed reads 2-way conflicts (rows p and p ^ 2 shared slot blocks):
+// SQ_LDS_BANK_CONFLICT per bf16 backward launch 2.16e8 -> 4.1e7 cycles, step 118.5 -> 117.5 ms (A/B,
+// profiles/r02/lds_swizzle_ab.log).  A full bit permutation of p that is equally conflict-free cost 26 more
+// instructions and a spill: 121.6 ms.
+__host__ __device__ constexpr int timg_perm(int p) { return p ^ ((p & 2) << 2); }
 __device__ __forceinline__ int timg_off(int p, int ch) { return p * HP + 4 * (ch ^ timg_perm(p)); }
 
 template <int NP>
@@ -708,7 +591,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   // fragment f of the shared image, or its register copy (index i in FwdRegs order)
   auto W = [&](int f, int i) -> Fr8<NP> {
-    if constexpr (REGW && NP == 2 && VISSM_FWD_X2 == 1) {  // hi planes from registers, lo planes from LDS
+    if constexpr (REGW && NP == 2) {  // hi planes from registers, lo planes from LDS
       Fr8<NP> r;
       r.h = wr->f[i].h;
       r.l = sh.img[f][1][lane];
@@ -722,7 +605,7 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   // layer 0: the MFMA accumulates onto C + theta (its C operand), so no separate add
   f4 acc[4];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) acc[ob] = VISSM_ACC_INIT ? X[ob] : f4{0.f, 0.f, 0.f, 0.f};
+  for (int ob = 0; ob < 4; ++ob) acc[ob] = X[ob];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     const Fr8<NP> uf = u_frag<NP>(uw, a.s, kb, g, c);
@@ -733,10 +616,10 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(VISSM_ACC_INIT ? acc[rb][r] : acc[rb][r] + X[rb][r]) : 0.f;
+      X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r]) : 0.f;
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
-    fence_uf<IMG, 6>();
+    fence_uf<IMG>();
     if (g == 3) X[3][3] = 1.f;  // the ones row: bias of layer l (and its gradient)
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) acc[ob] = f4{0.f, 0.f, 0.f, 0.f};
@@ -754,41 +637,32 @@ __device__ __forceinline__ void unit_forward(const KArgs& a, const Shared<NH, KB
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG || VISSM_BWD_MED3>(acc[rb][r]) : 0.f;
+      for (int r = 0; r < 4; ++r) X[rb][r] = 4 * rb + r < NR ? elu_fast<!IMG>(acc[rb][r]) : 0.f;
   }
   // head (16 output rows, o = 0: mu, o = 1: sigma pre-softplus; bias on the ones row)
-  fence_uf<IMG, 7>();
+  fence_uf<IMG>();
   if (g == 3) X[3][3] = 1.f;
   const int fh = 16 * NH + 4 * KB + 2 * JB;
   f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) d = mm<NP>(W(fh + ks, 8 * NH + 4 * KB + ks), chain_frag<NP>(X, ks), d);
-  if constexpr (VISSM_HEAD_REP) {
-    mu = d[0];
-    rr = d[1];
-  } else {
-    mu = __shfl(d[0], c, 64);
-    rr = __shfl(d[1], c, 64);
-  }
+  mu = d[0];
+  rr = d[1];
 }
 
 // ---------------------------------------------------------------------------
 // forward kernel: one work item (sample group x t-chunk) per wave; samples outer
 // ---------------------------------------------------------------------------
 template <int NH, int KB, int JB, int NP>
-#ifndef VISSM_FWD_OCC
-#define VISSM_FWD_OCC 2
-#endif
-__global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
+__global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                     const int32_t* __restrict__ win, const float* __restrict__ tht,
                                                     const bf8* __restrict__ img, const float* __restrict__ cst,
                                                     float* __restrict__ u_next, float* __restrict__ ls_slab) {
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][UW];
   load_shared(sh, img, cst);
-  if constexpr (VISSM_FWD_PRIO == 1) {
-    if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
-  } else if constexpr (VISSM_FWD_PRIO == 3) {
+  // static wave priority = dispatch round mod 4 (four blocks per CU; see bwd_kernel): 9.45 -> 9.15 ms per launch
+  {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
     if (r == 1) __builtin_amdgcn_s_setprio(1);
     else if (r == 2) __builtin_amdgcn_s_setprio(2);
@@ -802,8 +676,6 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
   float* uw = uwin[w];
-#if VISSM_FWD_REGW
-  constexpr bool REGW = NP != 2 || VISSM_FWD_X2 != 2;
   FwdRegs<NH, KB, NP> wr;
 #pragma unroll
   for (int i = 0; i < 8 * NH; ++i) wr.f[i] = wfrag(sh, i, lane);
@@ -811,20 +683,15 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
   for (int i = 0; i < 4 * KB; ++i) wr.f[8 * NH + i] = wfrag(sh, 16 * NH + i, lane);
 #pragma unroll
   for (int i = 0; i < 2; ++i) wr.f[8 * NH + 4 * KB + i] = wfrag(sh, 16 * NH + 4 * KB + 2 * JB + i, lane);
-#else
-  constexpr bool REGW = false;
-  const FwdRegs<NH, KB, NP> wr{};
-#endif
-  const int lwi = (VISSM_LANE_SCALARS && win && lane < nb) ? win[b_lo + lane] : 0;
+  const int lwi = (win && lane < nb) ? win[b_lo + lane] : 0;
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     const float* ub = u + static_cast<size_t>(b) * a.L;
     float* ob = u_next + static_cast<size_t>(b) * a.Lout;
-    const int wi = VISSM_LANE_SCALARS ? lane_i(lwi, bl) : (win ? win[b] : 0);
+    const int wi = lane_i(lwi, bl);
     const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
     float ls = 0.f;
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
-      fence_fwd<false>();
       const int nP = min(P, m_hi - m0), t0 = a.s * m0;
       f4 X[4];
       float mu, rr;
@@ -834,7 +701,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nP, X);
         stage_win<KB>(wn, uw, nullptr);
       }
-      unit_forward<NH, KB, JB, NP, false, REGW>(a, sh, uw, X, mu, rr, nullptr, nullptr, &wr);
+      unit_forward<NH, KB, JB, NP, false, true>(a, sh, uw, X, mu, rr, nullptr, nullptr, &wr);
       if (g == 0 && c < nP) {
         const float sg = softplus_fast(rr) + 1e-10f;
         const int oq = a.s * c + (a.s - 1);
@@ -844,7 +711,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD_OCC) void fwd_kernel(KArgs a, const f
           const int oe = t0 + 2 * c;
           ob[a.swap_out ? (oe ^ 1) : oe] = uw[2 * c + a.k];
         }
-        if (o >= a.Lout - a.n_logsig) ls += VISSM_FWD_HWLOG ? __builtin_amdgcn_logf(sg) * kLn2 : logf(sg);
+        if (o >= a.Lout - a.n_logsig) ls += __builtin_amdgcn_logf(sg) * kLn2;
       }
     }
     const float v = wave_sum(ls);
@@ -872,12 +739,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   constexpr int NPL = NP == 3 ? 2 : 1;
   constexpr int KP = 16 * JB;  // carry slots (k <= KP)
   constexpr int NS = NH + 1;   // images: I_0 .. I_NH (reused for dZ_l and dA0)
-  constexpr bool GI = VISSM_BWD_GIMG && NH == 1;
-  constexpr bool I0R = VISSM_BWD_I0REG && NH == 1 && NP == 1;
+  constexpr bool GI = NH == 1;              // the head gradient rides in the dZ image
+  constexpr bool I0R = NH == 1 && NP == 1;  // elu'(I_0) from the recompute's bf16 pairs in registers
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW][NS][NPL][P * HP];  // [wave][slot][plane][p][h]
   __shared__ float dthl[NW][S][DTH];
-  __shared__ __attribute__((aligned(16))) float dths[NW][4];  // (VISSM_BWD_DTHRMW) sink for the rows beyond DTH
+  __shared__ __attribute__((aligned(16))) float dths[NW][4];  // sink for the d theta rows beyond DTH
   __shared__ float carry[NW][S][KP];
   __shared__ float gsc[NW][3][P];              // sigma, d r, go even (stride 2)
   __shared__ float uwin[NW][UW];
@@ -900,13 +767,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   // the wrap): 29.6 -> 28.8 ms per launch for the two-level (round & 1) form, 28.9 -> 28.8 more for mod 4;
   // by blockIdx parity (pairs of equal priority) no change; capped at 3 (ties from round 3 on) 29.5 ms;
   // by the wave's slot on its SIMD (hwreg HW_ID) 30.0 ms.
-  if constexpr (VISSM_BWD_PRIO == 1) {
-    if (__builtin_amdgcn_readfirstlane((blockIdx.x / a.ncu) & 1)) __builtin_amdgcn_s_setprio(1);
-  } else if constexpr (VISSM_BWD_PRIO >= 2) {
-    // the younger block of a pair wins: priority grows with the dispatch round (blocks / CUs), capped
-    // at 3 (VISSM_BWD_PRIO 2) or wrapping mod 4 (3)
-    int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu);
-    r = VISSM_BWD_PRIO == 2 ? (r < 3 ? r : 3) : (r & 3);
+  {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
     if (r == 1) __builtin_amdgcn_s_setprio(1);
     else if (r == 2) __builtin_amdgcn_s_setprio(2);
     else if (r == 3) __builtin_amdgcn_s_setprio(3);
@@ -921,27 +783,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int i = threadIdx.x; i < NW * KP * QW; i += NT) (&dscr[0][0][0])[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  // Work items (sample group x t-chunk), one per wave.  With a.dcb (one window) the block's NW
-  // waves take NW consecutive groups of the SAME chunk and sum their dC tiles through LDS at each
-  // tile's end (fixed order), so the dC slab holds one row per block of groups; otherwise a
-  // block's waves are independent and no block-level synchronisation follows.
-  int item, grp, chn;
-  if (a.dcb) {
-    chn = blockIdx.x % a.n_chunks;
-    grp = (blockIdx.x / a.n_chunks) * NW + w;
-    item = grp * a.n_chunks + chn;
-  } else {
-    item = blockIdx.x * NW + w;
-    grp = item / a.n_chunks;
-    chn = item % a.n_chunks;
-  }
-  item = __builtin_amdgcn_readfirstlane(item);  // wave-uniform: scalar loads of per-sample data
-  grp = __builtin_amdgcn_readfirstlane(grp);
-  chn = __builtin_amdgcn_readfirstlane(chn);
-  const bool valid = grp < a.n_groups;
-  if (!a.dcb && !valid) return;  // (dcb: an idle wave still joins the block's tile barriers)
+  // Work items (sample group x t-chunk), one per wave; a block's waves are independent (no block-level
+  // synchronisation follows)
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);  // wave-uniform: scalar loads of per-sample data
+  const int grp = item / a.n_chunks, chn = item % a.n_chunks;
+  if (grp >= a.n_groups) return;
   const int m_lo = chn * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
-  const int b_lo = grp * a.S, nb = valid ? min(a.S, a.B - b_lo) : 0;
+  const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
   __bf16* ih[NS];
   __bf16* il[NS];
 #pragma unroll
@@ -969,10 +817,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
   for (int i = 0; i < 4; ++i) dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
   const bf4 ones4 = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
-  const int fwc = 16 * NH + 4 * KB, fis = 16 * NH + 4 * KB + 2 * JB + 2;
+  const int fwc = 16 * NH + 4 * KB;
 
-  const int lwi = (VISSM_LANE_SCALARS && win && lane < nb) ? win[b_lo + lane] : 0;
-  const float ldl = (!FZ && VISSM_LANE_SCALARS && lane < nb) ? dls[b_lo + lane] : 0.f;
+  const int lwi = (win && lane < nb) ? win[b_lo + lane] : 0;
+  const float ldl = (!FZ && lane < nb) ? dls[b_lo + lane] : 0.f;
   float lt0 = 0.f, lt1 = 0.f, lis = 0.f;  // FZ: theta_0, theta_1, e^{-theta_2} of sample b_lo + lane
   if constexpr (FZ) {
     if (lane < nb) {
@@ -992,11 +840,11 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
     for (int bl = 0; bl < nb; ++bl) {
-      fence_bwd<0>();
+      fence();
       const int b = b_lo + bl;
-      const int wi = VISSM_LANE_SCALARS ? lane_i(lwi, bl) : (win ? win[b] : 0);
+      const int wi = lane_i(lwi, bl);
       const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
-      const float dl = FZ ? -fz.scale : (VISSM_LANE_SCALARS ? lane_f(ldl, bl) : dls[b]);
+      const float dl = FZ ? -fz.scale : lane_f(ldl, bl);
       f4 XN[4];
       float mu, rr;
       float fz_yp = 0.f, fz_bp = 0.f;  // FZ: the observation of x_t (row t - 1), loaded with the unit's inputs
@@ -1011,8 +859,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nZ, XN);
         stage_win<KB>(wn, uw, gw);
       }
-      // FZ (VISSM_FZ_ZCEARLY): the previous tile's last x read with the unit's inputs, not after the recompute
-      const float fz_zc = (FZ && VISSM_FZ_ZCEARLY) ? zcar[w][bl] : 0.f;
+      // FZ: the previous tile's last x read with the unit's inputs, not after the recompute
+      const float fz_zc = FZ ? zcar[w][bl] : 0.f;
       u2 i0p[4];
       unit_forward<NH, KB, JB, NP, true>(a, sh, uw, XN, mu, rr, ih, il, nullptr, I0R ? i0p : nullptr);
       // I_NH (the head input) with its ones row -> image NH, for dW_head
@@ -1028,7 +876,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const float x = uw[c + a.k] * sig + mu;
         float xp = row_prev(x);
         const float xn = row_next(x);
-        if (c == 0) xp = VISSM_FZ_ZCEARLY ? fz_zc : zcar[w][bl];
+        if (c == 0) xp = fz_zc;
         if (discard) {
           if (lane == PO - 1) zcar[w][bl] = x;
           continue;
@@ -1059,12 +907,12 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       float dsig = gmu * uw[oq + a.k];
       if (pv && t0 + oq >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig);
       const float gr = dsig * sigmoid_fast(rr);
-      if (VISSM_BWD_UNCOND || g == 0) {
+      if (g == 0) {
         gsc[w][0][c] = sig;
         if constexpr (!GI) gsc[w][1][c] = gr;
         if (a.s == 2) gsc[w][2][c] = pv ? gw[2 * c] : 0.f;
       }
-      fence_bwd<1>();
+      fence();
       // GI: the head gradient G rides in two padding rows of the dZ image (below); the I_NH
       // fragments of dW_head are read now, before that image overwrites I_NH's slot
       Fr4<NP> i1f[4];
@@ -1082,30 +930,24 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           gv4[jj] = c == 0 ? g0 : (c == 1 ? g1 : 0.f);
         }
         const Fr4<NP> gf = split4<NP>(gv4);
-        if (!(kAbl & 1))
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(ih[NH], il[NH], hb, g, c), gf, dWh[hb]);
+        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(tr_frag<NP>(ih[NH], il[NH], hb, g, c), gf, dWh[hb]);
       }
       // dZ_{NH-1} = (w~_mu gmu + w~_r gr) * elu'(I_NH) -> image NH: the rank-2 outer product is
       // one K = 16 MFMA per row block, A[h][o] = W~h[16 rb + h][o], B[o][p] = (gmu, gr)[o] at p = c
       // (only k-group g = 0 carries the two nonzero k rows)
-      // (VISSM_BWD_BATCHW, one hidden layer: the dX fragments read before the head-backward VALU)
+      // (one hidden layer: the dX weight fragments, dW's I_0 fragments and dW_eps's u fragments read before the
+      // head-backward VALU)
       Fr8<NP> wb[8];
-      Fr4<NP> xa0[4];  // (VISSM_BWD_BATCHW & 8: dW's I_0 fragments read here as well)
-      Fr4<NP> uaf[JB];  // (& 16: dW_eps's u fragments)
-      float cin_early = 0.f;  // (& 32: the transposed conv's carry-in)
-      if constexpr ((VISSM_BWD_BATCHW & 2) && NH == 1) {
+      Fr4<NP> xa0[4];
+      Fr4<NP> uaf[JB];
+      if constexpr (NH == 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) wb[i] = wfrag(sh, 8 * NH + i, lane);
-        if constexpr (VISSM_BWD_BATCHW & 8) {
 #pragma unroll
-          for (int ib = 0; ib < 4; ++ib) xa0[ib] = tr_frag<NP>(ih[0], il[0], ib, g, c);
-        }
-        if constexpr (VISSM_BWD_BATCHW & 16) {
+        for (int ib = 0; ib < 4; ++ib) xa0[ib] = tr_frag<NP>(ih[0], il[0], ib, g, c);
 #pragma unroll
-          for (int jb = 0; jb < JB; ++jb) uaf[jb] = ua_frag<NP>(uw, a.s, jb, g, c);
-        }
-        if constexpr (VISSM_BWD_BATCHW & 32) cin_early = mycarry[bl * KP + (lane < a.k ? lane : 0)];
+        for (int jb = 0; jb < JB; ++jb) uaf[jb] = ua_frag<NP>(uw, a.s, jb, g, c);
         __builtin_amdgcn_sched_barrier(0);
       }
       f4 D[4];
@@ -1113,23 +955,16 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const bool g0 = g == 0;
         const Fr4<NP> gf2 = split4<NP>(f4{g0 ? gmu : 0.f, g0 ? gr : 0.f, 0.f, 0.f});
         unsigned wvh[4], wvl[4];
-        if constexpr (VISSM_BWD_WHP) {
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb) {
-            wvh[rb] = whp[16 * rb + c];
-            if constexpr (NP == 3) wvl[rb] = whp[HP + 16 * rb + c];
-          }
+        for (int rb = 0; rb < 4; ++rb) {
+          wvh[rb] = whp[16 * rb + c];
+          if constexpr (NP == 3) wvl[rb] = whp[HP + 16 * rb + c];
         }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           Fr4<NP> wa;
-          if constexpr (VISSM_BWD_WHP) {
-            wa.h = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
-            if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u});
-          } else {
-            wa.h = __builtin_bit_cast(bf4, u2{g0 ? whp[16 * rb + c] : 0u, 0u});
-            if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? whp[HP + 16 * rb + c] : 0u, 0u});
-          }
+          wa.h = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
+          if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u});
           D[rb] = mm<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? D[rb][r] * elu_d(XN[rb][r]) : 0.f;
@@ -1142,23 +977,23 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
       }
       put_image<NP>(ih[NH], il[NH], D, g, c);
-      Fr8<NP> wcp[2 * JB];  // (VISSM_BWD_BATCHW & 4: the dcon fragments, read before elu'(I_0))
-      // (VISSM_BWD_DWLATE: the dZ image's four fragments; block 3 is also dW_head's B operand)
-      constexpr bool DWL = VISSM_BWD_DWLATE > 0 && NH == 1 && GI && (VISSM_BWD_BATCHW & 10) == 10;
+      Fr8<NP> wcp[2 * JB];  // (one hidden layer: the dcon fragments, read before elu'(I_0))
+      // (DWL, one hidden layer: the dW / dW_head MFMAs deferred past the du section's dcon stores, from the dZ
+      //  image's four fragments read at their usual place; block 3 is also dW_head's B operand)
+      constexpr bool DWL = NH == 1;
       Fr4<NP> dzf[4];
       auto dw_late = [&]() {
 #pragma unroll
-        for (int ib = 0; ib < 4 * !(kAbl & 2); ++ib)
+        for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob) dW[0][ib][ob] = mm<NP>(xa0[ib], dzf[ob], dW[0][ib][ob]);
-        if (!(kAbl & 1))
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], dzf[3], dWh[hb]);
+        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], dzf[3], dWh[hb]);
       };
       // hidden layers, top down: dI_l = W~_l dZ_l (chain); dW_l += I_l dZ_l^T; dZ_{l-1} = dI_l elu'(I_l)
 #pragma unroll
       for (int l = NH - 1; l >= 0; --l) {
-        fence_bwd<2>();
+        fence();
         f4 dX[4];
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) dX[ib] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1167,17 +1002,16 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
           for (int ib = 0; ib < 4; ++ib)
-            dX[ib] = mm<NP>(((VISSM_BWD_BATCHW & 2) && NH == 1) ? wb[ib * 2 + ks] : wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane),
-                            df, dX[ib]);
+            dX[ib] = mm<NP>(NH == 1 ? wb[ib * 2 + ks] : wfrag(sh, 8 * NH + l * 8 + ib * 2 + ks, lane), df, dX[ib]);
         }
-        fence_bwd<3>();
+        fence();
         if constexpr (DWL) {
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob) dzf[ob] = tr_frag<NP>(ih[1], il[1], ob, g, c);
         }
 #pragma unroll
-        for (int ib = 0; ib < 4 * !(kAbl & 2) * !DWL; ++ib) {
-          const Fr4<NP> xa = ((VISSM_BWD_BATCHW & 10) == 10 && NH == 1) ? xa0[ib] : tr_frag<NP>(ih[l], il[l], ib, g, c);
+        for (int ib = 0; ib < 4 * !DWL; ++ib) {
+          const Fr4<NP> xa = tr_frag<NP>(ih[l], il[l], ib, g, c);
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob)
             dW[l][ib][ob] = mm<NP>(xa, tr_frag<NP>(ih[l + 1], il[l + 1], ob, g, c), dW[l][ib][ob]);
@@ -1186,11 +1020,10 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           // dW_head[h][o] += sum_p I_1[h][p] G[o][p]: B = rows 48..63 of the dZ image, columns
           // c = 5, 6 of the product hold o = 0, 1 (padding rows 53, 54)
           const Fr4<NP> gb = tr_frag<NP>(ih[NH], il[NH], 3, g, c);
-          if (!(kAbl & 1))
 #pragma unroll
-            for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], gb, dWh[hb]);
+          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mm<NP>(i1f[hb], gb, dWh[hb]);
         }
-        if constexpr ((VISSM_BWD_BATCHW & 4) && NH == 1) {
+        if constexpr (NH == 1) {
 #pragma unroll
           for (int i = 0; i < 2 * JB; ++i) wcp[i] = wfrag(sh, fwc + i, lane);
           __builtin_amdgcn_sched_barrier(0);
@@ -1211,8 +1044,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         }
         if (l > 0) put_image<NP>(ih[l], il[l], D, g, c);
       }
-      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]; dC tile += dA0 (identity selection)
-      fence_bwd<4>();
+      // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p]; dC tile += dA0
+      fence();
       f4 dcn[JB];
 #pragma unroll
       for (int jb = 0; jb < JB; ++jb) dcn[jb] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1221,68 +1054,41 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
         const Fr8<NP> df = chain_frag<NP>(D, ks);
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb)
-          dcn[jb] = mm<NP>(((VISSM_BWD_BATCHW & 4) && NH == 1) ? wcp[jb * 2 + ks] : wfrag(sh, fwc + jb * 2 + ks, lane), df,
-                           dcn[jb]);
-        if constexpr (!VISSM_BWD_VALU_DC) {
-#pragma unroll
-          for (int o2 = 0; o2 < 2 * !(kAbl & 16); ++o2)
-            dCa[2 * ks + o2] = mm_ax<NP>(sh.img[fis + 2 * ks + o2][0][lane], df, dCa[2 * ks + o2]);
-        }
+          dcn[jb] = mm<NP>(NH == 1 ? wcp[jb * 2 + ks] : wfrag(sh, fwc + jb * 2 + ks, lane), df, dcn[jb]);
       }
-      if constexpr (VISSM_BWD_VALU_DC) {
-        // dC tile += dA0 (same lane layout): fp32 adds on the unit-carrying registers
+      // dC tile += dA0 (same lane layout): fp32 adds on the unit-carrying registers (an identity-selection MFMA
+      // measured slower in this kernel)
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (4 * rb + r < NR) dCa[rb][r] += D[rb][r];
-      }
+        for (int r = 0; r < 4; ++r)
+          if (4 * rb + r < NR) dCa[rb][r] += D[rb][r];
       // dA0 -> image 1; dW_eps and d theta from its position-contracted fragments
       put_image<NP>(ih[1], il[1], D, g, c);
-      if constexpr (DWL && VISSM_BWD_DWLATE == 1) dw_late();
-      fence_bwd<5>();
+      fence();
       f4 dth4[4] = {};
 #pragma unroll
-      for (int hb = 0; hb < 4 * !(kAbl & 4); ++hb) {
+      for (int hb = 0; hb < 4; ++hb) {
         const Fr4<NP> ta = tr_frag<NP>(ih[1], il[1], hb, g, c);
         dth4[hb] = mm_bx<NP>(ta, ones4, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb)
-          dWe[jb][hb] = mm<NP>(((VISSM_BWD_BATCHW & 18) == 18 && NH == 1) ? uaf[jb] : ua_frag<NP>(uw, a.s, jb, g, c), ta,
-                               dWe[jb][hb]);
+          dWe[jb][hb] = mm<NP>(NH == 1 ? uaf[jb] : ua_frag<NP>(uw, a.s, jb, g, c), ta, dWe[jb][hb]);
       }
-      if constexpr (DWL && VISSM_BWD_DWLATE == 2) dw_late();
-      if (VISSM_BWD_DTHRMW && !VISSM_BWD_DTHATOM && !VISSM_BWD_UNCOND) {
-        // the four read-modify-writes with their reads issued together: rows 16 hb + 4 g beyond DTH (hb = 3,
-        // g >= 2: padding and the ones row) go to a per-wave scratch slot instead of a branch around them
-        if (c == 0) {
-          float* base = &dthl[w][bl][4 * g];
-          f4* dp[4];
+      // the four read-modify-writes with their reads issued together: rows 16 hb + 4 g beyond DTH (hb = 3, g >= 2:
+      // padding and the ones row) go to a per-wave scratch slot instead of a branch around them (every column of
+      // dth4 holds the same sums)
+      if (c == 0) {
+        float* base = &dthl[w][bl][4 * g];
+        f4* dp[4];
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb)
-            dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
-          f4 o[4];
+        for (int hb = 0; hb < 4; ++hb)
+          dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
+        f4 o[4];
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
+        for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
 #pragma unroll
-          for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
-        }
-      } else if (VISSM_BWD_UNCOND || c == 0) {  // (every column of dth4 holds the same sums)
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb) {
-          if (16 * hb + 4 * g < DTH) {
-            if constexpr (VISSM_BWD_DTHATOM) {
-              // no-return LDS adds: nothing waits on them (one lane per address: a fixed order)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                __hip_atomic_fetch_add(&dthl[w][bl][16 * hb + 4 * g + r], dth4[hb][r], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-              f4* dp = reinterpret_cast<f4*>(&dthl[w][bl][16 * hb + 4 * g]);
-              *dp = *dp + dth4[hb];
-            }
-          }
-        }
+        for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
       }
       if constexpr (DU) {
 #pragma unroll
@@ -1293,13 +1099,13 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           dsc[j * QW + (PADDED ? a.s * c + j : c)] = dcn[jb][r];
         }
       }
-      if constexpr (DWL && VISSM_BWD_DWLATE == 3) dw_late();
+      if constexpr (DWL) dw_late();
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       if constexpr (DU) {
         float* db = du + static_cast<size_t>(b) * a.L;
         // fin + k <= 64 when PADDED (k <= 32), <= 96 otherwise
         constexpr int NBASE = PADDED ? 1 : 2;
-        const int lim = kAbl & 8 ? 0 : fin + a.k;
+        const int lim = fin + a.k;
 #pragma unroll
         for (int it = 0; it < NBASE; ++it) {
           const int base = 64 * it;
@@ -1308,23 +1114,18 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           float v = 0.f;
           if constexpr (PADDED) {
             const int qc = q < QW ? q : QW - 1;
-            if (VISSM_BWD_KFIX > 0 && a.k == VISSM_BWD_KFIX) {
-              constexpr int KF = VISSM_BWD_KFIX > 0 ? VISSM_BWD_KFIX : 1;
-              if constexpr (VISSM_BWD_DUTREE) {
-                // all KF reads issued before the first add, then a pairwise sum (a chain of serial adds had
-                // the compiler wait on each read in turn)
-                float t[KF];
+            if (a.k == 8) {
+              // k = 8 (the AR configurations): all reads issued before the first add, then a pairwise sum (a chain of
+              // serial adds had the compiler wait on each read in turn)
+              constexpr int KF = 8;
+              float t[KF];
 #pragma unroll
-                for (int j = 0; j < KF; ++j) t[j] = dsc[j * QW + qc];
+              for (int j = 0; j < KF; ++j) t[j] = dsc[j * QW + qc];
 #pragma unroll
-                for (int w2 = 1; w2 < KF; w2 *= 2)
+              for (int w2 = 1; w2 < KF; w2 *= 2)
 #pragma unroll
-                  for (int j = 0; j + w2 < KF; j += 2 * w2) t[j] += t[j + w2];
-                v = t[0];
-              } else {
-#pragma unroll
-                for (int j = 0; j < KF; ++j) v += dsc[j * QW + qc];
-              }
+                for (int j = 0; j + w2 < KF; j += 2 * w2) t[j] += t[j + w2];
+              v = t[0];
             } else {
 #pragma unroll 4
               for (int j = 0; j < a.k; ++j) v += dsc[j * QW + qc];
@@ -1346,35 +1147,15 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
             if (a.s == 1) v += gw[oq2] * gsc[w][0][oq2];
             else v += (oq2 & 1) ? gw[oq2] * gsc[w][0][oq2 >> 1] : gsc[w][2][oq2 >> 1];
           }
-          const float cin = ((VISSM_BWD_BATCHW & 34) == 34 && NH == 1 && PADDED) ? cin_early
-                                                                                   : mycarry[bl * KP + (q < a.k ? q : 0)];
+          const float cin = mycarry[bl * KP + (q < a.k ? q : 0)];
           if (q < a.k) v += cin;
           if (q < fin) db[t0 + q] = v;
           else if (q < fin + a.k) mycarry[bl * KP + q - fin] = v;
         }
       }
-      if constexpr (DWL && VISSM_BWD_DWLATE == 4) dw_late();
     }
-    // tile done: its dC over the group (dcb: over the block's groups, summed through the waves'
-    // image slots -- free until the next unit -- in wave order)
-    if (a.dcb) {
-      float* mine = reinterpret_cast<float*>(&timg[w][0][0][0]);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * rb + r < NR) mine[(4 * rb + r) * 64 + lane] = dCa[rb][r];
-      __syncthreads();
-      float* dcs = dC_slab + (static_cast<size_t>(blockIdx.x / a.n_chunks) * a.Lh + m0) * a.H;
-      for (int i = w; i < NR; i += NW) {  // register row i of every lane
-        float s = 0.f;
-#pragma unroll
-        for (int v = 0; v < NW; ++v) s += reinterpret_cast<const float*>(&timg[v][0][0][0])[i * 64 + lane];
-        const int h = swz(16 * (i >> 2) + 4 * g + (i & 3));
-        if (c < nP && h < a.H) dcs[c * a.H + h] = s * kLog2e;
-      }
-      __syncthreads();
-    } else if (c < nP) {
+    // tile done: its dC over the group
+    if (c < nP) {
       const size_t row = (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
       if (a.dc16) {  // (bf16 partials: each rounding is independent, the reduce sums 4096 of them in fp32)
         __bf16* dcs = reinterpret_cast<__bf16*>(dC_slab) + row;
@@ -1398,7 +1179,6 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     }
   }
 
-  if (!valid) return;
   if constexpr (FZ) {
     if (lane < nb) {  // lane bl: its sample's columns in order
       float v = 0.f;
@@ -1481,67 +1261,28 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 constexpr int NW2 = 8;
 constexpr int NT2 = 64 * NW2;
 constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
-#ifndef VISSM_BWD2
-#define VISSM_BWD2 1
-#endif
-#ifndef VISSM_BWD2_FENCE
-#define VISSM_BWD2_FENCE 2  // compiler fences between the unit's phases: 1 always, 0 never, 2 in the fused (FZ)
-                            // variant only (A/B, AR-cfg launches: middle flows 23.3 -> 22.4 ms without them, the
-                            // fused one 26.8 -> 28.2, the first flow unchanged)
-#endif
-#ifndef VISSM_BWD2_MED3
-#define VISSM_BWD2_MED3 1  // the recompute's ELU select as v_med3 (one instruction fewer per element): 93.3 -> 91.4 ms
-                           // per AR-cfg step (A/B); in the one-sample kernel it measured slower
-#endif
-#ifndef VISSM_BWD2_FZ_BRANCH
-#define VISSM_BWD2_FZ_BRANCH 0  // 0: a t-chunk's look-back tile (fused variant) runs the whole unit with every
-                                // gradient zero (nP = 0 masks them) instead of branching out after the recompute:
-                                // the branch split the unit into basic blocks the scheduler cannot interleave across
-#endif
+// Design decisions (A/B, AR-cfg launches):
+//  * compiler fences between the unit's phases in the fused (FZ) variant only (without them: middle flows 23.3 ->
+//    22.4 ms, the fused one 26.8 -> 28.2, the first flow unchanged);
+//  * the recompute's ELU select as v_med3 (one instruction fewer per element): 93.3 -> 91.4 ms per AR-cfg step;
+//  * a t-chunk's look-back tile (fused variant) runs the whole unit with every gradient zero (nP = 0 masks them): a
+//    branch out after the recompute split the unit into basic blocks the scheduler cannot interleave across;
+//  * the dC tile summed by a K = 32 MFMA over the pair's dA0 image fragments against a position-selection B operand
+//    instead of fp32 VALU adds of the dA0 accumulators (-0.4 ms per step);
+//  * dW_eps accumulated transposed ([h][tap]) by one K = 32 MFMA per row block whose B operand's columns 8..15 carry
+//    one-hot sample columns: the same product sums d theta for 8 samples, flushed to the LDS rows every fourth pair
+//    (4 MFMAs and 3 of 4 read-modify-writes fewer per pair; -1.7 ms per step);
+//  * fused variant: the tile's observations (per position) loaded once per tile; log sigma on v_log_f32 (sigma >=
+//    1e-10 is a normal float); per-sample log sigma column sums in LDS at bf16 (through two padding rows of the dA0
+//    image into the merged dW_eps / d theta product in the split-weight recompute variant, whose lo weight planes
+//    take that LDS; no change at bf16).
+// Rejected: elu'(I_1) = min(2^x', 1) from the recompute's exp kept to the head backward (+1 ms per step: registers);
+// per-sample d theta for the whole item in a [h][16 samples] MFMA accumulator (16 more registers: 60 spilled);
+// s_setprio 1 for the second wave on each SIMD (-0.2 ms, noise).
 template <bool FZ>
 __device__ __forceinline__ void fence2() {
-  if constexpr (VISSM_BWD2_FENCE == 1 || (VISSM_BWD2_FENCE == 2 && FZ)) fence();
+  if constexpr (FZ) fence();
 }
-#ifndef VISSM_BWD2_ELUE
-#define VISSM_BWD2_ELUE 0  // elu'(I_1) = min(2^x', 1) from the recompute's exp (kept in registers to the head
-                           // backward) instead of re-derived from I_1 (med3 + fma per element)
-#endif
-#ifndef VISSM_BWD2_DCMF
-#define VISSM_BWD2_DCMF 1  // the dC tile summed by a K = 32 MFMA over the pair's dA0 image fragments (a position
-                           // selection B operand) instead of fp32 VALU adds of the dA0 accumulators
-#endif
-#ifndef VISSM_BWD2_DTMF
-#define VISSM_BWD2_DTMF 0  // per-sample d theta accumulated for the whole item by a K = 32 MFMA against a one-hot
-                           // sample operand into a [h][16 samples] accumulator (16 VGPRs) instead of per-pair LDS
-                           // read-modify-writes of [S][DTH] rows (28 KB of LDS per block freed)
-#endif
-#ifndef VISSM_BWD2_DWT
-#define VISSM_BWD2_DWT 1  // dW_eps accumulated transposed ([h][tap]) by one K = 32 MFMA per row block whose B operand's
-                          // columns 8..15 carry one-hot sample columns: the same product also sums d theta for 8
-                          // samples, flushed to the LDS rows every fourth pair (4 MFMAs and 3 of 4 read-modify-writes
-                          // fewer per pair)
-#endif
-#ifndef VISSM_BWD2_FZLS
-#define VISSM_BWD2_FZLS 0  // fused variant: the per-sample log sigma sums through two padding rows of the dA0 image into
-                           // the merged dW_eps / d theta product instead of per-pair LDS read-modify-writes of [S][16]
-                           // column sums (no change at bf16, A/B; always on in the split-weight recompute variant, whose
-                           // lo weight planes take that LDS)
-#endif
-#ifndef VISSM_BWD2_PRIO
-#define VISSM_BWD2_PRIO 0  // 1: waves 4-7 (the second wave on each SIMD) at s_setprio 1
-#endif
-#ifndef VISSM_BWD2_FZTILE
-#define VISSM_BWD2_FZTILE 1  // fused variant: the tile's observations (per position, not per sample) loaded once per
-                             // tile instead of with every pair's inputs
-#endif
-#ifndef VISSM_BWD2_FZLOG
-#define VISSM_BWD2_FZLOG 1  // fused variant: log sigma on v_log_f32 (sigma >= 1e-10 is a normal float: __logf's
-                            // denormal scaling is dead code)
-#endif
-#ifndef VISSM_BWD2_FZDIAG
-#define VISSM_BWD2_FZDIAG 0  // timing-only ablations of the fused variant's own work (results wrong when set): 1 no x
-                             // stores, 2 no log sigma sums, 4 no obs loads, 8 no AR(1) stencil (upstream gradient 0)
-#endif
 
 // the K = 32 fragment of a position contraction: sample A's transposed fragment then sample B's
 __device__ __forceinline__ bf8 cat8(bf4 a, bf4 b) {
@@ -1567,15 +1308,14 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW2][2][2 * P * HP];  // [wave][slot][row 16 cb + position][64 h]
-  __shared__ float dthl[NW2][VISSM_BWD2_DTMF ? 1 : S][DTH];
+  __shared__ float dthl[NW2][S][DTH];
   __shared__ __attribute__((aligned(16))) float dths[NW2][4];
   __shared__ float carry[NW2][S][KP2];
   __shared__ float gsc[NW2][2][P];
   __shared__ float uwin[NW2][2][64];
   __shared__ float gwin[NW2][2][P];
   __shared__ float dscr[NW2][2][KP2][QW2];
-  constexpr bool ZLS = FZ && !VISSM_BWD2_FZLS && NPR == 1;  // per-column log sigma sums in LDS
-  static_assert(!FZ || ZLS || VISSM_BWD2_DWT, "the log sigma sums without LDS ride in the merged dW_eps / d theta product");
+  constexpr bool ZLS = FZ && NPR == 1;  // per-column log sigma sums in LDS
   __shared__ float zls[ZLS ? NW2 : 1][ZLS ? S : 1][P];
   __shared__ bf8 slo[NPR == 2 ? 14 : 1][64];  // NPR = 2: lo planes of WF 0..7, WE 0..3, WH 0..1
   __shared__ float zcar[FZ ? NW2 : 1][FZ ? S : 1];
@@ -1590,16 +1330,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   } else {
     load_shared<NH, KB, JB, NP, NT2>(sh, img, cst);
   }
-  if constexpr (VISSM_BWD2_PRIO == 1) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-  }
   if constexpr (FZ) {
     if constexpr (ZLS)
       for (int i = threadIdx.x; i < NW2 * S * P; i += NT2) (&zls[0][0][0])[i] = 0.f;
     for (int i = threadIdx.x; i < NW2 * S; i += NT2) (&zcar[0][0])[i] = 0.f;
   }
-  if constexpr (!VISSM_BWD2_DTMF)
-    for (int i = threadIdx.x; i < NW2 * S * DTH; i += NT2) (&dthl[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NW2 * S * DTH; i += NT2) (&dthl[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW2 * S * KP2; i += NT2) (&carry[0][0][0])[i] = 0.f;
   for (int i = threadIdx.x; i < NW2 * 2 * KP2 * QW2; i += NT2) (&dscr[0][0][0][0])[i] = 0.f;
   __syncthreads();
@@ -1615,22 +1351,15 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   const unsigned* whp = reinterpret_cast<const unsigned*>(&sh.cst[NH * HP]);  // (mu, r) bf16 pairs
 
   f4 dW[4][4], dWe[4], dWh[4];
-  f4 DT[4];  // VISSM_BWD2_DTMF: d theta of the group's 16 samples, [h][sample] (lane (g, c): sample c)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) dW[i][o] = f4{0.f, 0.f, 0.f, 0.f};
     dWe[i] = f4{0.f, 0.f, 0.f, 0.f};
     dWh[i] = f4{0.f, 0.f, 0.f, 0.f};
-    DT[i] = f4{0.f, 0.f, 0.f, 0.f};
   }
   const int fwc = 16 * NH + 4 * KB;
-  // d theta's ones operand, split by sample: B[k = 8g + jj][n = c] = 1 if position k belongs to the sample of
-  // column block n (columns 0-7: sample A = jj < 4, columns 8-15: sample B)
-  bf8 ones_ab;
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) ones_ab[jj] = (__bf16)(((jj < 4) == (c < 8)) ? 1.f : 0.f);
-  // VISSM_BWD2_DCMF: B[k = 8g + jj][n = c] = 1 if k's position 4g + (jj & 3) is column n (either sample)
+  // the dC selection operand: B[k = 8g + jj][n = c] = 1 if k's position 4g + (jj & 3) is column n (either sample)
   bf8 sel_p;
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) sel_p[jj] = (__bf16)((4 * g + (jj & 3) == c) ? 1.f : 0.f);
@@ -1654,8 +1383,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
     f4 dCa[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) dCa[rb] = f4{0.f, 0.f, 0.f, 0.f};
-    float fz_yt = 0.f, fz_bt = 0.f;  // FZ (VISSM_BWD2_FZTILE): the observation of x_t (row t - 1) at p = c
-    if constexpr (FZ && VISSM_BWD2_FZTILE && !(VISSM_BWD2_FZDIAG & 4)) {
+    float fz_yt = 0.f, fz_bt = 0.f;  // FZ: the observation of x_t (row t - 1) at p = c, once per tile
+    if constexpr (FZ) {
       const int wo = min(max(m0 + c - 1, 0), fz.M - 1);
       fz_yt = fz.obs[wo];
       fz_bt = fz.bin[wo];
@@ -1680,11 +1409,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           }
         }
         if (!two) gv[1] = 0.f;
-        if constexpr (FZ && !VISSM_BWD2_FZTILE && !(VISSM_BWD2_FZDIAG & 4)) {
-          const int wo = min(max(m0 + c - 1, 0), fz.M - 1);
-          fz_yp = fz.obs[wo];
-          fz_bp = fz.bin[wo];
-        }
         const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nZ)) * HP) + g;
         f4 cr[4], tr[2][4];
         if constexpr (TF) {  // the theta fold: the pair's theta rows of the layer-0 B operand (lane groups 2, 3)
@@ -1715,7 +1439,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       // ---- forward recompute of both samples (shared weight fragments)
       u2 i0p[2][4];
-      f4 E1[2][4];  // VISSM_BWD2_ELUE: elu'(I_1)
       float mu[2], rr[2];
       {
         f4 acc[2][4];
@@ -1742,7 +1465,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2_MED3>(acc[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         fence2<FZ>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1774,21 +1497,13 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2_MED3>(acc[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         fence2<FZ>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
           if (g == 3) X[cb][3][3] = 1.f;
-        if constexpr (VISSM_BWD2_ELUE) {
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) E1[cb][rb][r] = fminf(__builtin_amdgcn_exp2f(acc[cb][rb][r]), 1.f);
-        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const Fr8<NP> wf = wfrag(sh, fh + ks, lane);
@@ -1819,11 +1534,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           const float xn = row_next(x);
           if (c == 0) xp = fz_zc[cb];
           const int bl2 = blv[cb];
-          if (VISSM_BWD2_FZ_BRANCH && discard) {
-            if (lane == PO - 1 && (cb == 0 || two)) zcar[w][bl2] = x;
-            gmu[cb] = 0.f;
-            continue;
-          }
           const float th0 = lane_f(lt0, bl2), th1 = lane_f(lt1, bl2), is = lane_f(lis, bl2);
           const int t = m0 + c;
           const float fh = (pv && t < fz.M) ? 1.f : 0.f;
@@ -1832,15 +1542,13 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           const float zt = fh * (xn - th1 * x - th0) * is;
           const float zp = ft * (x - th1 * xp - th0) * is;
           const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
-          gmu[cb] = (cb == 0 || two) && !(VISSM_BWD2_FZDIAG & 8) ? -fz.scale * de : 0.f;
-          const float lsg = (t0 + c >= a.Lout - a.n_logsig)
-                                ? (VISSM_BWD2_FZLOG ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : __logf(sig[cb]))
-                                : 0.f;
+          gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
+          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : 0.f;
           if (g == 0) {
             gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the rest of the unit reads
             if (pv && (cb == 0 || two)) {
-              if constexpr (!(VISSM_BWD2_FZDIAG & 1)) fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
-              if constexpr (!(VISSM_BWD2_FZDIAG & 2) && ZLS) zls[w][bl2][c] += lsg;
+              fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
+              if constexpr (ZLS) zls[w][bl2][c] += lsg;
             }
           }
           if constexpr (!ZLS) lsv[cb] = (pv && (cb == 0 || two)) ? lsg : 0.f;
@@ -1849,7 +1557,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           gmu[cb] = pv ? gwin[w][cb][c] : 0.f;
         }
       }
-      if (VISSM_BWD2_FZ_BRANCH && discard) continue;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const float dl = FZ ? -fz.scale : lane_f(ldl, blv[cb]);
@@ -1898,7 +1605,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * (VISSM_BWD2_ELUE ? E1[cb][rb][r] : elu_d(X[cb][rb][r])) : 0.f;
+              D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
           put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
         }
       }
@@ -1952,13 +1659,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int cb = 0; cb < 2; ++cb) dcn[cb] = mm<NP>(wc, chain_frag<NP>(D[cb], ks), dcn[cb]);
         }
       }
-      if constexpr (!VISSM_BWD2_DCMF) {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (4 * rb + r < NR) dCa[rb][r] += D[0][rb][r] + D[1][rb][r];
-      }
       if constexpr (FZ && !ZLS) {
         // the log sigma of the pair's output columns rides in two padding rows of the dA0 image (register (3, 1):
         // row 49 = unit 52 <- hi, row 53 = unit 53 <- lo of a split-bf16 pair), so the merged dW_eps / d theta
@@ -1982,39 +1682,30 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       fence2<FZ>();
       // dW_eps and d theta from dA0's position-contracted fragments (K = 32)
-      f4 dth4[4];
       {
-        // VISSM_BWD2_DTMF: B[k][n] = 1 if k's sample (jj >> 2: A, B) is group sample n
-        const unsigned one2 = 0x3F803F80u, sa = c == blv[0] ? one2 : 0u, sb = (two && c == blv[1]) ? one2 : 0u;
-        const bf8 selb = __builtin_bit_cast(bf8, u4{sa, sa, sb, sb});
+        const unsigned one2 = 0x3F803F80u;
         bf8 uaf;
         {
           const Fr4<NP> ua = ua_frag<NP>(uwin[w][0], 1, 0, g, c), ub = ua_frag<NP>(uwin[w][1], 1, 0, g, c);
           uaf = cat8(ua.h, ub.h);
         }
-        // VISSM_BWD2_DWT: one B operand for dW_eps^T (columns j < 8: the u windows) and the d theta of the pair's
-        // two samples (columns 8 + slot: one-hot by sample, slot = sample mod 8)
+        // one B operand for dW_eps^T (columns j < 8: the u windows) and the d theta of the pair's two samples
+        // (columns 8 + slot: one-hot by sample, slot = sample mod 8)
         bf8 bcomb = uaf;
-        if constexpr (VISSM_BWD2_DWT) {
+        {
           const unsigned ta_ = c - 8 == (blv[0] & 7) ? one2 : 0u, tb_ = (two && c - 8 == (blv[1] & 7)) ? one2 : 0u;
           if (c >= 8) bcomb = __builtin_bit_cast(bf8, u4{ta_, ta_, tb_, tb_});
         }
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
           const bf8 ta = tr_frag2(im1, hb, g, c);
-          if constexpr (VISSM_BWD2_DWT) {
-            dWe[hb] = mfma32(ta, bcomb, dWe[hb]);
-          } else {
-            if constexpr (VISSM_BWD2_DTMF) DT[hb] = mfma32(ta, selb, DT[hb]);
-            else dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
-            dWe[hb] = mfma32(uaf, ta, dWe[hb]);
-          }
-          if constexpr (VISSM_BWD2_DCMF) dCa[hb] = mfma32(ta, sel_p, dCa[hb]);
+          dWe[hb] = mfma32(ta, bcomb, dWe[hb]);
+          dCa[hb] = mfma32(ta, sel_p, dCa[hb]);
         }
       }
-      // VISSM_BWD2_DWT: the eight sample columns flushed into the per-sample d theta rows after every fourth pair
-      // and after the tile's last, then cleared
-      if constexpr (VISSM_BWD2_DWT) {
+      // the eight sample columns flushed into the per-sample d theta rows after every fourth pair and after the
+      // tile's last, then cleared
+      {
         if ((bl & 7) == 6 || bl + 2 >= nb) {
           const int smp = (bl & ~7) + c - 8;
           if (c >= 8 && smp < nb) {
@@ -2033,19 +1724,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int hb = 0; hb < 4; ++hb)
             if (c >= 8) dWe[hb] = f4{0.f, 0.f, 0.f, 0.f};
         }
-      }
-      // per-sample d theta read-modify-writes: lane c = 0 (sample A) and c = 8 (sample B)
-      if (!VISSM_BWD2_DTMF && !VISSM_BWD2_DWT && (c == 0 || (c == 8 && two))) {
-        float* base = &dthl[w][c == 0 ? blv[0] : blv[1]][4 * g];
-        f4* dp[4];
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb)
-          dp[hb] = reinterpret_cast<f4*>(16 * hb + 4 * g < DTH ? base + 16 * hb : &dths[w][0]);
-        f4 o[4];
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb) o[hb] = *dp[hb];
-#pragma unroll
-        for (int hb = 0; hb < 4; ++hb) *dp[hb] = o[hb] + dth4[hb];
       }
       // du over local positions q in [0, nP + k) for both samples at once: lane = 32 cb + q
       if constexpr (DU) {
@@ -2117,20 +1795,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + lane] = v;
       }
     }
-    if (!VISSM_BWD2_DTMF && lane < a.H)
-      dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
-  }
-  if constexpr (VISSM_BWD2_DTMF) {
-    if (c < nb) {
-      float* row = dth_slab + (static_cast<size_t>(chn) * a.B + b_lo + c) * a.H;
-#pragma unroll
-      for (int hb = 0; hb < 4; ++hb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int h = swz(16 * hb + 4 * g + r);
-          if (h < a.H) row[h] = DT[hb][r] * kLog2e;
-        }
-    }
+    if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
   }
 
   // weight-gradient partials of this work item (the layout of bwd_kernel's)
@@ -2140,12 +1805,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 4 * g + r, h = swz(16 * hb + c);
-      if constexpr (VISSM_BWD2_DWT) {  // dWe^T: lane column c = tap, rows h
-        const int ht = swz(16 * hb + 4 * g + r);
-        if (c < a.k && ht < H) ws[c * H + ht] = dWe[hb][r] * kLog2e;
-      } else if (j < a.k && h < H) ws[j * H + h] = dWe[hb][r] * kLog2e;
+    for (int r = 0; r < 4; ++r) {  // dWe^T: lane column c = tap, rows h
+      const int ht = swz(16 * hb + 4 * g + r);
+      if (c < a.k && ht < H) ws[c * H + ht] = dWe[hb][r] * kLog2e;
     }
   const int off_w = a.k * H, off_b = off_w + NH * H * H;
 #pragma unroll
@@ -2178,29 +1840,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // ---------------------------------------------------------------------------
 // forward kernel, two samples per unit ("fwd2"): the AR configurations' shape (one hidden layer, bf16, k <= 16,
 // stride 1, one window).  Pairs of samples outer, tiles inner: the pair's two chains run interleaved in one
-// wave and share the tile's C rows and every weight fragment (register-resident with VISSM_FWD2_REGW).
+// wave and share the tile's C rows and every weight fragment (register-resident).  It also runs the three-hidden-
+// layer forward (LV / FHN heads, k <= 32; SV's 32 < k <= 64 at stride 1 with two layer-0 K blocks and a 128-entry u
+// window) and the bf16x2 forward of the parity-precision modes.
 // ---------------------------------------------------------------------------
-#ifndef VISSM_FWD2
-#define VISSM_FWD2 1
-#endif
-#ifndef VISSM_THETA_FOLD
-#define VISSM_THETA_FOLD 1  // the two-sample AR kernels form the theta term in the layer-0 product (fold_ok)
-#endif
-#ifndef VISSM_FWD2N
-#define VISSM_FWD2N 1  // the three-hidden-layer forward (LV / FHN heads, k <= 32) on the two-sample kernel
-#endif
-#ifndef VISSM_FWD2_K64
-#define VISSM_FWD2_K64 1  // and for 32 < k <= 64 at stride 1 (SV: two layer-0 K blocks, 128-entry u window)
-#endif
-#ifndef VISSM_FWD2_X2
-#define VISSM_FWD2_X2 1  // the bf16x2 forward (parity-precision modes) runs the two-sample kernel too
-#endif
-#ifndef VISSM_FWD2_REGW
-#define VISSM_FWD2_REGW 1
-#endif
-#ifndef VISSM_FWD2_OCC
-#define VISSM_FWD2_OCC 2
-#endif
 // TF: the theta fold (VissmFlowParams.theta_rank): the theta term rides in the layer-0 product's K rows 16..31
 // (lane groups 2, 3 of the B operand: the sample's fragment thf[b][g - 2], loaded once per pair) instead of a
 // [64] theta_term row per sample and tile added to the C rows
@@ -2209,7 +1852,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // NH / JB: one hidden layer (AR) or three with the BN affine folded (LV / SV / FHN heads: stride-2 head with the
 // pass-through of the even outputs and the fused pair swap), k <= 32 (one layer-0 K block)
 template <bool TF, int NP, int NH, int JB>
-__global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const float* __restrict__ u,
+__global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
                                                                   const bf8* __restrict__ img,
@@ -2221,7 +1864,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ float uwin[NW][2][64 * KB];
   load_shared(sh, img, cst);
-  if constexpr (VISSM_FWD_PRIO == 3) {
+  {  // static wave priority = dispatch round mod 4 (as fwd_kernel)
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
     if (r == 1) __builtin_amdgcn_s_setprio(1);
     else if (r == 2) __builtin_amdgcn_s_setprio(2);
@@ -2234,21 +1877,18 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
   const int grp = item / a.n_chunks, ch = item % a.n_chunks;
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
-  constexpr int NWR = VISSM_FWD2_REGW ? 8 * NH + 4 * KB + 2 : 1;
+  constexpr int NWR = 8 * NH + 4 * KB + 2;
   bf8 wr[NWR];
-  if constexpr (VISSM_FWD2_REGW) {
 #pragma unroll
-    for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
+  for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
 #pragma unroll
-    for (int i = 0; i < 4 * KB; ++i) wr[8 * NH + i] = sh.img[16 * NH + i][0][lane];
+  for (int i = 0; i < 4 * KB; ++i) wr[8 * NH + i] = sh.img[16 * NH + i][0][lane];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
-  }
-  // fragment f of the shared image, or its register copy (index i); NP = 2: with its lo plane from LDS
+  for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
+  // fragment f: its hi plane's register copy (index i); NP = 2: with its lo plane from LDS
   auto W = [&](int f, int i) -> Fr8<NP> {
     Fr8<NP> r;
-    if constexpr (VISSM_FWD2_REGW) r.h = wr[i];
-    else r.h = sh.img[f][0][lane];
+    r.h = wr[i];
     if constexpr (NP == 2) r.l = sh.img[f][1][lane];
     return r;
   };
@@ -2373,7 +2013,7 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
             const int oe = t0 + 2 * c;
             ob[swp ? (oe ^ 1) : oe] = uwin[w][cb][2 * c + a.k];
           }
-          if (o >= a.Lout - a.n_logsig) ls[cb] += VISSM_FWD_HWLOG ? __builtin_amdgcn_logf(sg) * kLn2 : logf(sg);
+          if (o >= a.Lout - a.n_logsig) ls[cb] += __builtin_amdgcn_logf(sg) * kLn2;
         }
       }
     }
@@ -2398,15 +2038,6 @@ __global__ __launch_bounds__(NT, VISSM_FWD2_OCC) void fwd2_kernel(KArgs a, const
 // ---------------------------------------------------------------------------
 constexpr int NW3 = 4;
 constexpr int NT3 = 64 * NW3;
-#ifndef VISSM_BWD2N
-#define VISSM_BWD2N 1
-#endif
-#ifndef VISSM_BWD2N_MED3
-#define VISSM_BWD2N_MED3 1
-#endif
-#ifndef VISSM_BWD2N_K64
-#define VISSM_BWD2N_K64 1  // the two-sample kernel also for 32 < k <= 64 (SV's k = 50), stride 1
-#endif
 
 __device__ __forceinline__ void put_pairs(__bf16* img, const u2 (&v)[4], int g, int c) {
 #pragma unroll
@@ -2540,7 +2171,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2N_MED3>(acc[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
           fence();
@@ -2569,7 +2200,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
             for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<VISSM_BWD2N_MED3>(acc[cb][rb][r]) : 0.f;
+                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         }
         fence();
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -2884,13 +2515,11 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 // ---------------------------------------------------------------------------
 struct Geom {
   int s, Lout, Lh, S, n_groups, n_tiles, CH, n_chunks, n_items;
-  int dcb, n_dc;  // block-summed dC tiles (backward, one window); dC slab rows
-  int blocks;     // grid size
+  int blocks;  // grid size of the 4-wave kernels
 };
 
-#ifndef VISSM_TARGET_ITEMS
-#define VISSM_TARGET_ITEMS 8192  // work items (sample group x t-chunk) a launch aims for
-#endif
+// work items (sample group x t-chunk) a launch aims for (4096 / 12288 / 16384: within +-0.3 ms at the AR-cfg shape)
+constexpr int kTargetItems = 8192;
 static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   Geom g;
   g.s = d->stride2 ? 2 : 1;
@@ -2901,8 +2530,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   g.n_tiles = (g.Lh + po - 1) / po;
   int ch_min_tiles = ((d->k + g.s - 1) / g.s + po - 1) / po;
   if (ch_min_tiles < 1) ch_min_tiles = 1;
-  const int target_items = VISSM_TARGET_ITEMS;
-  int want = (target_items + g.n_groups - 1) / g.n_groups;
+  int want = (kTargetItems + g.n_groups - 1) / g.n_groups;
   int max_chunks = g.n_tiles / ch_min_tiles;
   if (max_chunks < 1) max_chunks = 1;
   int nc = want < max_chunks ? want : max_chunks;
@@ -2913,9 +2541,7 @@ static Geom geom(const VissmFlowDesc* d, bool backward, int po = P) {
   g.CH = tiles_per_chunk * po;
   g.n_chunks = (g.Lh + g.CH - 1) / g.CH;
   g.n_items = g.n_groups * g.n_chunks;
-  g.dcb = (backward && d->n_win == 1 && VISSM_BWD_DCB) ? 1 : 0;
-  g.n_dc = g.dcb ? (g.n_groups + NW - 1) / NW : g.n_groups;
-  g.blocks = g.dcb ? g.n_dc * g.n_chunks : (g.n_items + NW - 1) / NW;
+  g.blocks = (g.n_items + NW - 1) / NW;
   return g;
 }
 
@@ -2953,7 +2579,7 @@ static size_t ws_layout(const VissmFlowDesc* d, const Geom& g, bool backward, ch
   if (!backward) {
     t.ls_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * 4));
   } else {
-    t.dC_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_dc) * g.Lh * d->H * 4));
+    t.dC_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_groups) * g.Lh * d->H * 4));
     t.dth_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_chunks) * d->B * d->H * 4));
     t.dW_slab = reinterpret_cast<float*>(take(static_cast<size_t>(g.n_items) * n_wgrad(d) * 4));
     t.halo = reinterpret_cast<float*>(take(static_cast<size_t>(d->B) * g.n_chunks * d->k * 4));
@@ -2981,9 +2607,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
-  a.dcb = g.dcb;
-  a.dc16 = (VISSM_BWD_DC16 && !g.dcb && d->n_win == 1 &&
-            (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2)) ? 1 : 0;
+  a.dc16 = (d->n_win == 1 && (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2)) ? 1 : 0;
   a.ncu = device_cus();
   return a;
 }
@@ -3036,31 +2660,27 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowPar
   }
 }
 
-#ifndef VISSM_BWD2_X2
-#define VISSM_BWD2_X2 1  // the fused last flow at VISSM_PREC_BF16X2 (bf16x2f): split-weight recompute in bwd2_kernel
-#endif
 // the two-sample backward covers the AR configurations' flow shape
 static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_BWD2 && d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
-         d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S && !g.dcb;
+  return d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
+         d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
 }
 
 // the three-hidden-layer two-sample backward: LV / FHN heads (k <= 24: padded dcon rows), SV (32 < k <= 64, stride 1:
 // the diagonal du sum), one window
 static bool bwd2n_ok(const VissmFlowDesc* d, const Geom& g) {
-  return VISSM_BWD2N && d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 &&
-         (d->k <= 24 || (VISSM_BWD2N_K64 && d->k > 32 && d->k <= 64 && !d->stride2)) && d->H <= kMaxH &&
-         d->n_win == 1 &&
-         g.S == S && !g.dcb;
+  return d->precision == VISSM_PREC_BF16 && d->n_hidden == 3 &&
+         (d->k <= 24 || (d->k > 32 && d->k <= 64 && !d->stride2)) && d->H <= kMaxH && d->n_win == 1 && g.S == S;
 }
 
 // the two-sample forward covers the AR configurations' flow shape
 static bool fwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  if (!VISSM_FWD2 || d->H > kMaxH || d->n_win != 1 || g.S != S || d->k > 64) return false;
-  if (d->k > 32 && (d->n_hidden != 3 || d->stride2 || !VISSM_FWD2_K64)) return false;  // two K blocks: SV's shape
-  if (d->n_hidden == 1) return !d->bn && !d->stride2 && !d->swap_out && (d->precision == VISSM_PREC_BF16 ||
-                                                                        (VISSM_FWD2_X2 && d->precision == VISSM_PREC_BF16X2));
-  return VISSM_FWD2N && d->n_hidden == 3 && d->precision == VISSM_PREC_BF16;
+  if (d->H > kMaxH || d->n_win != 1 || g.S != S || d->k > 64) return false;
+  if (d->k > 32 && (d->n_hidden != 3 || d->stride2)) return false;  // two K blocks: SV's shape
+  if (d->n_hidden == 1)
+    return !d->bn && !d->stride2 && !d->swap_out &&
+           (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2);
+  return d->n_hidden == 3 && d->precision == VISSM_PREC_BF16;
 }
 
 }  // namespace VISSM_FLOW5_NS
@@ -3138,7 +2758,7 @@ void VISSM_FLOW5_API(flow5_geometry)(const VissmFlowDesc* d, int which, int32_t*
 // the caller supplied the theta branch's factors (VissmFlowParams.theta_rank) and the shape leaves K rows 16..31 of
 // the layer-0 product free
 static bool fold_ok(const VissmFlowDesc* d, const VissmFlowParams* w) {
-  return VISSM_THETA_FOLD && w->theta_rank >= 1 && w->theta_rank <= 5 && w->theta_x && w->w_theta && w->b_theta &&
+  return w->theta_rank >= 1 && w->theta_rank <= 5 && w->theta_x && w->w_theta && w->b_theta &&
          d->k <= kFoldRow && d->n_hidden == 1;
 }
 
@@ -3264,8 +2884,8 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {
-    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_dc, nC, st)
-                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
+    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_groups, nC, st)
+                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_groups, nC, st);
     if (rc) return rc;
   } else {
     rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
@@ -3288,7 +2908,7 @@ bool VISSM_FLOW5_API(flow5_ar_fused_supports)(const VissmFlowDesc* d) {
   const bool shape = d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH &&
                      d->n_win >= 1;
   if (d->precision == VISSM_PREC_BF16X2)  // split-weight recompute: the two-sample kernel's shape only
-    return VISSM_BWD2_X2 && shape && d->k <= KP2 && d->n_win == 1;
+    return shape && d->k <= KP2 && d->n_win == 1;
   return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && shape;
 }
 
@@ -3319,7 +2939,7 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
   const bool x2 = d->precision == VISSM_PREC_BF16X2;
   // bf16x2 has only the two-sample kernel: it must meet that kernel's geometry (bwd2_ok minus the precision test)
-  VISSM_CHECK_ARG(!x2 || (g.S == S && !g.dcb && d->n_win == 1 && d->k <= KP2),
+  VISSM_CHECK_ARG(!x2 || (g.S == S && d->n_win == 1 && d->k <= KP2),
                   "flow_ar_elbo_fused: bf16x2 needs the two-sample kernel's geometry (one window, k <= %d)", KP2);
   const bool b2 = x2 || bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
   launch_prep(d, w, ws, fold, st);
@@ -3357,8 +2977,8 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {
-    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_dc, nC, st)
-                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_dc, nC, st);
+    rc = a.dc16 ? launch_reduce_rows_bf16(ws.dC_slab, dC, g.n_groups, nC, st)
+                : launch_reduce_rows_inplace(ws.dC_slab, dC, g.n_groups, nC, st);
   } else {
     rc = launch_reduce_by_window(ws.dC_slab, win, dC, d->B, d->n_win, nC, st);
   }

@@ -63,6 +63,25 @@ class _ThetaBranch(torch.autograd.Function):
         return dtheta, dW0, sW2 @ W1.t(), dW1, sW2, dW2, s
 
 
+class _SumGradOverRanks(torch.autograd.Function):
+    """Identity forward; the backward SUM-all-reduces the incoming gradient over the data-parallel ranks.  Placed
+    on the window-shared conv output C (and the sample-channel slice of the same conv kernel) when every rank
+    holds the same windows: the window-shared backward (feature MLP, conv over features -- LV's 31.8 M
+    parameters) is linear in dC, so running it replicated on the summed dC gives every rank the full-batch
+    gradient of those parameters with a [n_win, Lh, H] all-reduce per flow instead of theirs (vi_ssm.py)."""
+
+    @staticmethod
+    def forward(ctx, x, dist_ctx):
+        ctx.dist = dist_ctx
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().clone()
+        ctx.dist.all_reduce_(g)
+        return g, None
+
+
 class _DiagSum(torch.autograd.Function):
     """C[w, m, :] = sum_j G[w, s m + j, j, :] (the valid conv's diagonal gather).  The backward
     writes dC into the (non-overlapping) diagonal of a zero dG with one strided copy instead of
@@ -230,9 +249,20 @@ class IAF:
             bn_g = bn_b = None
         return w_eps, w_hid, b_hid, bn_g, bn_b, self._p("head/kernel"), self._p("head/bias")
 
-    def flow(self, shape: FlowShape, win, u, C, theta_term, tf=None):
+    def shared_grad_names(self) -> List[str]:
+        """Variables whose gradient reaches them only through the window-shared conv output C and the sample
+        channel of the first conv kernel: the feature MLP and the first conv (its kernel's channel 0 is w_eps)."""
+        return [f"{self.pre}/feat{j}/{t}" for j in range(4) for t in ("kernel", "bias")] + \
+            [f"{self.pre}/conv/kernel", f"{self.pre}/conv/bias"]
+
+    def flow(self, shape: FlowShape, win, u, C, theta_term, tf=None, grad_sum=None):
+        """grad_sum (a DistCtx): C and w_eps enter through _SumGradOverRanks (their gradients summed over the
+        ranks inside the backward, see Engine.grad_sum)."""
         s = self.spec
         w_eps = self._p("conv/kernel")[:, 0, :].contiguous()
+        if grad_sum is not None:
+            C = _SumGradOverRanks.apply(C, grad_sum)
+            w_eps = _SumGradOverRanks.apply(w_eps, grad_sum)
         if s.n_hidden > 0:
             w_hid = torch.stack([self._p(f"hidden{l}/kernel") for l in range(s.n_hidden)])
             b_hid = torch.stack([self._p(f"hidden{l}/bias") for l in range(s.n_hidden)])
@@ -313,6 +343,9 @@ class Engine:
         # tiles per t-chunk forced on every flow launch (VissmFlowDesc.chunk_tiles; 0 = automatic): parity tests
         # run a large batch's launch geometry at a small batch
         self.chunk_tiles = 0
+        # data parallelism: a DistCtx here makes forward() route each flow's C and w_eps through
+        # _SumGradOverRanks (set per step by VISSMBase when every rank holds the same windows)
+        self.grad_sum = None
         H = mdef.network_dims[0]
         if any(h != H for h in mdef.network_dims):
             raise ValueError("all network_dims must be equal (the reference adds layer outputs of width network_dims[0])")
@@ -407,7 +440,7 @@ class Engine:
                               stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
                               n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
                               chunk_tiles=self.chunk_tiles)
-            u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta))
+            u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta), grad_sum=self.grad_sum)
             lq = lq - ls
             L -= md.k
         z = u

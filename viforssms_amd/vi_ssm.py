@@ -88,6 +88,10 @@ class VISSMBase:
         self.skip_nonfinite = bool(skip_nonfinite)
         # >1 ranks: all-reduce each flow's gradient bucket as soon as its backward completes (overlap)
         self.overlap_allreduce = True
+        # >1 ranks on the same windows: all-reduce each flow's dC instead of its window-shared variables' gradients
+        # where that is fewer bytes (_shared_grad_plan; LV)
+        self.shared_dc_allreduce = True
+        self.last_allreduce_bytes = 0
         self.T = mdef.scale_num
         self.batch_dims = mdef.M
         self._batch_cache: Dict[tuple, Batch] = {}
@@ -121,16 +125,46 @@ class VISSMBase:
         return int(self.T)
 
     def batch_for(self, starts_global: np.ndarray) -> Batch:
+        """This rank's batch of the step's window starts (all ranks' draws).  Also records whether every rank
+        holds the same distinct windows (each rank replays the same draw, so this needs no communication): then
+        the window-shared gradients can be summed through dC (_shared_grad_plan)."""
         r = self.dist.rank
-        local = np.asarray(starts_global[r * self.p_local:(r + 1) * self.p_local], dtype=np.int64)
+        starts_global = np.asarray(starts_global, dtype=np.int64)
+        local = starts_global[r * self.p_local:(r + 1) * self.p_local]
         uniq = np.unique(local)
+        same = all(np.array_equal(np.unique(starts_global[q * self.p_local:(q + 1) * self.p_local]), uniq)
+                   for q in range(self.dist.world))
         key = (tuple(uniq.tolist()) if len(uniq) == 1 else None)
         if key is not None and key in self._batch_cache and self._batch_cache[key].B == len(local):
-            return self._batch_cache[key]
-        b = self.engine.make_batch(local)
-        if key is not None:
-            self._batch_cache = {key: b}
+            b = self._batch_cache[key]
+        else:
+            b = self.engine.make_batch(local)
+            if key is not None:
+                self._batch_cache = {key: b}
+        b.ranks_same_windows = same
         return b
+
+    # ------------------------------------------------------------------ window-shared gradients over ranks
+    def _shared_grad_plan(self, batch: Batch, fused: bool) -> bool:
+        """Sum the window-shared gradients through dC (Engine.grad_sum) on this step?  Needs >1 ranks holding the
+        same windows (batch_for) and the unfused step, and pays when the flows' dC ([n_win, Lh, H] each) is
+        smaller than the variables it replaces in the all-reduce: LV (31.8 M parameters, 127 MB, vs 3 x 1 MB of
+        dC at the LV-cfg shape), not AR (its window-shared variables are smaller than its dC).  A captured step
+        keeps the single blocking all-reduce of every gradient."""
+        if (self.dist.world <= 1 or fused or not getattr(batch, "ranks_same_windows", False)
+                or not self.shared_dc_allreduce
+                or (self.store.grad.is_cuda and torch.cuda.is_current_stream_capturing())):
+            return False
+        md = self.mdef
+        s = 2 if md.D == 2 else 1
+        n_dc = sum(batch.n_win * ((md.kernel_ext - (i + 1) * md.k) // s) * fl.spec.H + fl.spec.k * fl.spec.H
+                   for i, fl in enumerate(self.engine.flows))
+        n_shared = sum(self.store.offsets[n][1] for fl in self.engine.flows for n in fl.shared_grad_names())
+        self._plan_dc_numel = n_dc   # dC and w_eps gradients all-reduced inside the backward
+        return n_dc < n_shared
+
+    def _shared_names(self):
+        return {n for fl in self.engine.flows for n in fl.shared_grad_names()}
 
     # ------------------------------------------------------------------ one step
     def _draws(self, batch: Batch, step: int, eps=None, x0_theta=None, row0_dev=None):
@@ -155,7 +189,9 @@ class VISSMBase:
         """grad of sum(-ELBO) (AR.py:228-229) -> all-reduce -> clip_by_global_norm -> Adamax (AR.py:230-234)."""
         st = self.store
         st.zero_grad()
-        if self.engine.fused_ok(batch, batch.B):
+        fused = self.engine.fused_ok(batch, batch.B)
+        shared = self._shared_grad_plan(batch, fused)
+        if fused:
             # the last flow fused with the AR(1) ELBO terms (one kernel instead of the flow's forward and
             # backward and the ELBO's dz); the multi-root backward carries the same gradient of sum(-ELBO)
             e, bl, x0 = self._draws(batch, step, eps, x0_theta, row0_dev)
@@ -164,15 +200,19 @@ class VISSMBase:
             torch.autograd.backward(roots, grads)
             del roots, grads
         else:
-            out = self.forward(batch, step, eps, x0_theta, row0_dev)
+            self.engine.grad_sum = self.dist if shared else None
+            try:
+                out = self.forward(batch, step, eps, x0_theta, row0_dev)
+            finally:
+                self.engine.grad_sum = None
             loss = (-out["elbo"]).sum()
-            self._arm_overlap()
+            self._arm_overlap(shared)
             loss.backward()
             del loss
         # drop the autograd graph now: its parameter-accumulation nodes would otherwise live on into
         # the next step (and, under graph capture, run on the stream they were created on)
         out = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
-        self._reduce_grads()
+        self._reduce_grads(shared)
         if apply:
             o = self._opt_main
             gn = o.kernel.step(st.flat, st.grad, o.v, o.m, self.learn_rate, 0.95, 0.999, 1e-8, self.clip_norm(),
@@ -195,13 +235,17 @@ class VISSMBase:
         return None
 
     # ------------------------------------------------------------------ gradient all-reduce
-    def _grad_buckets(self):
+    def _grad_buckets(self, exclude=()):
         """Per-flow buckets of the flat gradient (each flow's variables are contiguous: flow{i}/...), in the
         order the backward completes them (last flow first), then the rest (q(theta)'s MAF, complete only
-        at the end).  A flow's bucket is final once every one of its variables has accumulated."""
+        at the end).  A flow's bucket is final once every one of its variables has accumulated.  exclude:
+        variables left out (the window-shared ones when their gradient was summed through dC; they are a
+        prefix of each flow's range, so the buckets stay contiguous)."""
         st = self.store
         groups: Dict[str, List[str]] = {}
         for n in st.names():
+            if n in exclude:
+                continue
             key = n.split("/")[0] if n.startswith("flow") else "rest"
             groups.setdefault(key, []).append(n)
         out = []
@@ -214,53 +258,74 @@ class VISSMBase:
         flows = sorted((x for x in out if x[0] != "rest"), key=lambda x: -int(x[0][4:]))
         return flows + [x for x in out if x[0] == "rest"]
 
-    def _arm_overlap(self):
+    def _bucket_cfg(self, shared: bool):
+        """(buckets, owner) for the step's mode: every variable, or without the window-shared ones (shared)."""
+        cache = self.__dict__.setdefault("_ov_cfg", {})
+        if shared not in cache:
+            buckets = self._grad_buckets(self._shared_names() if shared else ())
+            owner = {n: bi for bi, (_, _, _, names) in enumerate(buckets[:-1]) for n in names}
+            cache[shared] = (buckets, owner)
+        return cache[shared]
+
+    def _arm_overlap(self, shared: bool = False):
         """Before a backward on >1 ranks: each flow bucket's SUM all-reduce is launched (async) from the
         post-accumulate hook of its last variable, so it runs over xGMI while the earlier flows' backward
-        kernels still execute (LV-cfg's 127 MB gradient); _reduce_grads waits for them."""
+        kernels still execute; _reduce_grads waits for them.  shared: the step sums the
+        window-shared gradients through dC, so their variables are in no bucket."""
         if (self.dist.world <= 1 or not self.overlap_allreduce
                 or (self.store.grad.is_cuda and torch.cuda.is_current_stream_capturing())):
             self._ov = None   # (a captured step keeps the single blocking all-reduce)
             return
         st = self.store
-        if getattr(self, "_ov_buckets", None) is None:
-            self._ov_buckets = self._grad_buckets()
-            self._ov_owner = {}
-            for bi, (_, a, b, names) in enumerate(self._ov_buckets[:-1]):
-                for n in names:
-                    self._ov_owner[n] = bi
+        if not getattr(self, "_ov_hooked", False):
+            for n in st.names():
+                if n.startswith("flow"):
                     st.tensors[n].register_post_accumulate_grad_hook(self._make_hook(n))
-        self._ov = {"left": [len(x[3]) for x in self._ov_buckets], "handles": {}, "bad": set()}
+            self._ov_hooked = True
+        buckets, owner = self._bucket_cfg(shared)
+        self._ov = {"left": [len(x[3]) for x in buckets], "handles": {}, "bad": set(), "buckets": buckets,
+                    "owner": owner}
 
     def _make_hook(self, name):
         def hook(t):
             ov = getattr(self, "_ov", None)
-            if ov is None:
+            if ov is None or name not in ov["owner"]:
                 return
-            bi = self._ov_owner[name]
+            bi = ov["owner"][name]
             a, sz = self.store.offsets[name]
             if t.grad is None or t.grad.data_ptr() != self.store.grad[a:a + sz].data_ptr():
                 ov["bad"].add(bi)   # autograd re-allocated this .grad: reduce the bucket after sync_grads
             ov["left"][bi] -= 1
             if ov["left"][bi] == 0 and bi not in ov["bad"]:
                 import torch.distributed as dist
-                _, lo, hi, _ = self._ov_buckets[bi]
+                _, lo, hi, _ = ov["buckets"][bi]
                 ov["handles"][bi] = dist.all_reduce(self.store.grad[lo:hi], op=dist.ReduceOp.SUM,
                                                     group=self.dist.group, async_op=True)
         return hook
 
-    def _reduce_grads(self):
+    def _reduce_grads(self, shared: bool = False):
+        """SUM the flat gradient over the ranks (the buckets the backward hooks launched, then the rest).
+        shared: the window-shared variables' gradients are already full-batch sums on every rank (summed
+        through dC inside the backward) and are left out.  Records last_allreduce_bytes."""
         st = self.store
         ov, self._ov = getattr(self, "_ov", None), None
         st.sync_grads()
-        if ov is None:
+        if self.dist.world <= 1:
+            self.last_allreduce_bytes = 0
+        elif ov is None and not shared:
             self.dist.all_reduce_(st.grad)
+            self.last_allreduce_bytes = 4 * st.grad.numel()
         else:
-            for h in ov["handles"].values():
+            buckets = ov["buckets"] if ov is not None else self._bucket_cfg(shared)[0]
+            handles = ov["handles"] if ov is not None else {}
+            for h in handles.values():
                 h.wait()
-            for bi, (_, lo, hi, _) in enumerate(self._ov_buckets):
-                if bi not in ov["handles"]:
+            for bi, (_, lo, hi, _) in enumerate(buckets):
+                if bi not in handles:
                     self.dist.all_reduce_(st.grad[lo:hi])
+            self.last_allreduce_bytes = 4 * sum(hi - lo for _, lo, hi, _ in buckets)
+            if shared:
+                self.last_allreduce_bytes += 4 * self._plan_dc_numel
         m = self.grad_mask()
         if m is not None:   # elementwise: commutes with the SUM over ranks
             st.grad.mul_(m)
