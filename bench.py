@@ -13,7 +13,8 @@ counted) divided by its average launch time, measured live with HIP events on th
 during the timed steps; mixed_roof_frac prices the same FLOPs with the vector terms at the fp32
 vector peak.  step_roofline: sum of every kernel's t_min under its own roof / measured step time.
 parity_precision: the same step timed at the precisions that hold the per-sample ELBO within 1e-4 of the
-oracle -- bf16x2f (split-weight forward), bf16x3f and bf16x3 (every product split; gradient within 1e-3 too).
+oracle -- bf16x2 (split weights in every weight product, forward and backward: gradient within 1e-3 too), bf16x2f
+(split-weight forward only), bf16x3f and bf16x3 (every operand split; gradient within 1e-3 too).
 cpu_baseline: the fp32 CPU restatement of the same step (oracle/, "port") on a bounded sample of
 trajectories, timed on this host, plus the AR plumbing config (p = 50, M = 50, k = 50) at true size.
 
@@ -36,8 +37,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "latent-state transitions/sec (batch_dims×T per step), AR(1) T=5000, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3, "bf16x3f": 2500.0, "bf16x2f": 2500.0}  # MI355X dense (MI355X_MICROARCH.md);
-# bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak
+PEAKS_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3, "bf16x3f": 2500.0, "bf16x2f": 2500.0,
+                "bf16x2": 2500.0 / 2}  # MI355X dense (MI355X_MICROARCH.md);
+# bf16x3 issues three bf16 MFMAs per product, so its ceiling is a third of the bf16 peak (bf16x2: two per weight
+# product; priced at half the peak)
 VALU_PEAK_TFLOPS = 157.3  # fp32 vector (packed FMA) peak
 
 
@@ -263,7 +266,7 @@ def parse_args(argv=None):
     ap.add_argument("--M", type=int, default=None,
                     help="AR window length (reference batch_dims of AR.main; default M = T, the BASELINE workload; "
                          "hyperparameters.txt's case is --B 50 --M 50 --k 50)")
-    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x2f"], default="bf16",
+    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16x2", "bf16x3", "bf16x3f", "bf16x2f"], default="bf16",
                     help="flow-kernel MFMA operand precision (BASELINE configs[1]: bf16); ELBO densities, "
                          "reductions and the optimizer are fp32 throughout")
     ap.add_argument("--graph", action="store_true",
@@ -357,6 +360,11 @@ def measure(args, ctx, dev, parity_line: bool):
     if parity_line and args.precision == "bf16" and args.model == "ar" and world == 1 and not args.graph:
         px = []
         for name, mode, note in (
+                ("bf16x2", _lib.VISSM_PREC_BF16X2,
+                 "every product with a weight operand as split-bf16 weights x bf16 activations (w_hi x + w_lo x), the "
+                 "forward, the backward's recompute and its chain (W dZ, w_eps dA0, the head backward) alike; "
+                 "weight-gradient products single bf16: per-sample ELBO within 1e-4 AND gradient within 1e-3 of the "
+                 "float64 oracle (tests/test_gpu_config_parity.py, tests/test_gpu_fused.py)"),
                 ("bf16x2f", _lib.VISSM_PREC_BF16X2F,
                  "forward flow products with split-bf16 weights (w_hi x + w_lo x: the weights' rounding, coherent "
                  "over a path, removed) and bf16 activations, backward products bf16 (the last flow fused with the "

@@ -43,9 +43,14 @@ extern "C" {
 #define VISSM_PREC_FP32 0     /* exact fp32 arithmetic */
 #define VISSM_PREC_BF16 1     /* bf16 MFMA operands, fp32 accumulation */
 #define VISSM_PREC_BF16X3 2   /* split-bf16 (hi/lo) MFMA operands: ~fp32 products */
-#define VISSM_PREC_BF16X2 3   /* forward only: split-bf16 weights, bf16 activations (two MFMAs per product);
-                                 vissm_flow_bwd rejects it; vissm_flow_ar_elbo_fused takes it for k <= 8 on one
-                                 window (its recompute -- x, log sigma -- on split weights, backward products bf16) */
+#define VISSM_PREC_BF16X2 3   /* split-bf16 weights, bf16 activations: every product with a weight operand as
+                                 w_hi x + w_lo x (two MFMAs), the forward, the backward's recompute and its chain
+                                 (W dZ, w_eps dA0, the head backward) alike; the weight-gradient products
+                                 (activation x gradient) single bf16.  ELBO within 1e-4 and gradient within 1e-3 of
+                                 the float64 oracle at the AR configurations (one hidden layer, k <= 32) */
+#define VISSM_PREC_BF16X2_BF16 4  /* vissm_flow_ar_elbo_fused only: the recompute (x, log sigma) on split weights,
+                                     the backward products bf16 -- the last flow of a step whose forward runs at
+                                     VISSM_PREC_BF16X2 and backward at VISSM_PREC_BF16 (k <= 8, one window) */
 
 const char* vissm_last_error(void);
 int vissm_version(void);

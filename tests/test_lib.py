@@ -42,22 +42,29 @@ def test_library_rejects_bad_shapes_without_gpu():
     assert rc < 0 and b"bad shape" in lib.vissm_last_error()
 
 
-def test_bf16x2_is_forward_only_without_gpu():
-    """VISSM_PREC_BF16X2 (split weights, bf16 activations) runs the forward kernel; the backward entry
-    points refuse it before touching the device (include/vissm.h)."""
+def test_bf16x2_precisions_without_gpu():
+    """VISSM_PREC_BF16X2 (split weights, bf16 activations) is a forward and backward precision with workspace on
+    both sides; VISSM_PREC_BF16X2_BF16 belongs to the fused last AR flow only and the other entry points refuse it
+    before touching the device (include/vissm.h)."""
     from viforssms_amd import _lib
     lib = _lib.load()
     d = _lib.FlowDesc(4, 40, 8, 50, 1, 0, 0, 0, 32, 1, _lib.VISSM_PREC_BF16X2, 0)
     assert lib.vissm_flow_workspace_size(ctypes.byref(d), 0) > 0
+    assert lib.vissm_flow_workspace_size(ctypes.byref(d), 1) > 0
+    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)) == 1
     buf = (ctypes.c_float * 64)()
     p = ctypes.cast(buf, ctypes.c_void_p).value
     w = _lib.FlowParams(*([p] * len(_lib.FlowParams._fields_)))
     gr = _lib.FlowGrads(*([p] * len(_lib.FlowGrads._fields_)))
-    rc = lib.vissm_flow_bwd(ctypes.byref(d), ctypes.byref(w), p, p, None, p, p, p, p, p, p, ctypes.byref(gr), p, 64,
+    dx = _lib.FlowDesc(4, 40, 8, 50, 1, 0, 0, 0, 32, 1, _lib.VISSM_PREC_BF16X2_BF16, 0)
+    rc = lib.vissm_flow_bwd(ctypes.byref(dx), ctypes.byref(w), p, p, None, p, p, p, p, p, p, ctypes.byref(gr), p, 64,
                             None)
-    assert rc < 0 and b"forward-only" in lib.vissm_last_error()
-    # the fused last AR flow takes it at the two-sample kernel's shape (split-weight recompute, bf16 backward products)
-    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d)) == 1
+    assert rc < 0 and b"vissm_flow_ar_elbo_fused only" in lib.vissm_last_error()
+    rc = lib.vissm_flow_fwd(ctypes.byref(dx), ctypes.byref(w), p, p, None, p, p, p, p, 64, None)
+    assert rc < 0 and b"vissm_flow_ar_elbo_fused only" in lib.vissm_last_error()
+    # the fused last AR flow takes both at the two-sample kernel's shape (k <= 8, one window)
+    assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(dx)) == 1
+    assert lib.vissm_flow_ar_elbo_fused_workspace_size(ctypes.byref(dx)) > 0
     d33 = _lib.FlowDesc(4, 60, 20, 50, 1, 0, 0, 0, 32, 1, _lib.VISSM_PREC_BF16X2, 0)   # k = 20: not that shape
     assert lib.vissm_flow_ar_elbo_fused_supported(ctypes.byref(d33)) == 0
     assert set(_lib.HOST_MODES) <= set(_lib.TRAIN_PRECISIONS.values())

@@ -17,7 +17,8 @@ LIB_PATH = os.environ.get("VISSM_LIB", os.path.join(_HERE, "libvissm.so"))
 VISSM_PREC_FP32 = 0
 VISSM_PREC_BF16 = 1
 VISSM_PREC_BF16X3 = 2
-VISSM_PREC_BF16X2 = 3   # forward kernels only: split-bf16 weights, bf16 activations
+VISSM_PREC_BF16X2 = 3   # split-bf16 weights, bf16 activations in every weight product (forward and backward)
+VISSM_PREC_BF16X2_BF16 = 4   # vissm_flow_ar_elbo_fused only: split-weight recompute, bf16 backward products
 # host-level modes (not C-ABI precisions): forward products at the first precision (the values that reach
 # the ELBO: ELBO within 1e-4 of the float64 oracle), backward products bf16 (gradients at bf16 accuracy)
 VISSM_PREC_BF16X3F = 16   # forward bf16x3
@@ -26,7 +27,7 @@ HOST_MODES = {VISSM_PREC_BF16X3F: (VISSM_PREC_BF16X3, VISSM_PREC_BF16),
               VISSM_PREC_BF16X2F: (VISSM_PREC_BF16X2, VISSM_PREC_BF16)}
 # training-step precision modes by name (main.py / bench.py --precision, tests)
 TRAIN_PRECISIONS = {"fp32": VISSM_PREC_FP32, "bf16": VISSM_PREC_BF16, "bf16x3": VISSM_PREC_BF16X3,
-                    "bf16x3f": VISSM_PREC_BF16X3F, "bf16x2f": VISSM_PREC_BF16X2F}
+                    "bf16x2": VISSM_PREC_BF16X2, "bf16x3f": VISSM_PREC_BF16X3F, "bf16x2f": VISSM_PREC_BF16X2F}
 
 MODEL_AR, MODEL_LV, MODEL_SV, MODEL_FHN = 0, 1, 2, 3
 

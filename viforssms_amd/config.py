@@ -120,8 +120,10 @@ def handle_opts(argv=None):
                              "the launched world must equal N.  Default: the launcher's world (1 without one)")
     parser.add_argument("--steps", type=int, default=None, help="Stop after this many runs (default: endless)")
     parser.add_argument("--seed", type=int, default=1, help="Philox seed of the base noise")
-    parser.add_argument("--precision", choices=["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x2f"], default="fp32",
-                        help="flow products: fp32 exact, bf16, bf16x3 (split operands); bf16x3f / bf16x2f: "
+    parser.add_argument("--precision", choices=["fp32", "bf16", "bf16x2", "bf16x3", "bf16x3f", "bf16x2f"],
+                        default="fp32",
+                        help="flow products: fp32 exact, bf16, bf16x2 (split weights, bf16 activations, forward and "
+                             "backward), bf16x3 (split operands); bf16x3f / bf16x2f: "
                              "bf16x3 / split-weight forward products with bf16 backward products")
     parser.add_argument("--no-pretrain", action="store_true", help="Skip the 501 pre-training runs")
     parser.add_argument("--log-every", type=int, default=1)

@@ -59,7 +59,8 @@ static int validate(const VissmFlowDesc* d) {
   VISSM_CHECK_ARG(d->n_logsig >= 0 && d->n_logsig <= d->L - d->k, "flow: bad n_logsig");
   VISSM_CHECK_ARG(d->n_win >= 1, "flow: n_win must be >= 1");
   VISSM_CHECK_ARG(d->precision == VISSM_PREC_FP32 || d->precision == VISSM_PREC_BF16 ||
-                      d->precision == VISSM_PREC_BF16X3 || d->precision == VISSM_PREC_BF16X2,
+                      d->precision == VISSM_PREC_BF16X3 || d->precision == VISSM_PREC_BF16X2 ||
+                      d->precision == VISSM_PREC_BF16X2_BF16,
                   "flow: unknown precision %d", d->precision);
   VISSM_CHECK_ARG(d->chunk_tiles >= 0, "flow: chunk_tiles=%d must be >= 0 (0 = automatic)", d->chunk_tiles);
   return VISSM_OK;
@@ -113,6 +114,8 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                   "flow_fwd: null weight pointer");
   VISSM_CHECK_ARG(!d->bn || d->n_hidden == 0 || (w->bn_g && w->bn_b), "flow_fwd: bn needs bn_g/bn_b");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_fwd: n_win > 1 needs win[]");
+  VISSM_CHECK_ARG(d->precision != VISSM_PREC_BF16X2_BF16,
+                  "flow_fwd: VISSM_PREC_BF16X2_BF16 is a precision of vissm_flow_ar_elbo_fused only");
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
     return (use_nh3(d) ? flow5_fwd_nh3 : flow5_fwd)(d, w, u, C, win, theta_term, u_next, logsig, workspace,
@@ -129,8 +132,8 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   if (rc) return rc;
   VISSM_CHECK_ARG(w && u && C && theta_term && du_next && dlogsig && dC && dtheta_term && gr,
                   "flow_bwd: null pointer");
-  VISSM_CHECK_ARG(d->precision != VISSM_PREC_BF16X2,
-                  "flow_bwd: VISSM_PREC_BF16X2 is a forward-only precision (run the backward at VISSM_PREC_BF16)");
+  VISSM_CHECK_ARG(d->precision != VISSM_PREC_BF16X2_BF16,
+                  "flow_bwd: VISSM_PREC_BF16X2_BF16 is a precision of vissm_flow_ar_elbo_fused only");
   VISSM_CHECK_ARG(du || use_v5(d), "flow_bwd: du may be NULL only on the bf16 / bf16x3 kernels");
   VISSM_CHECK_ARG(gr->w_eps && gr->w_head && gr->b_head && (d->n_hidden == 0 || (gr->w_hid && gr->b_hid)),
                   "flow_bwd: null grad pointer");
@@ -163,7 +166,8 @@ int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, c
   int rc = validate(d);
   if (rc) return rc;
   VISSM_CHECK_ARG(flow5_ar_fused_supports(d),
-                  "flow_ar_elbo_fused: needs bf16 / bf16x3 (k <= 32) or bf16x2 (k <= 8, one window), one hidden layer, no BN, "
+                  "flow_ar_elbo_fused: needs bf16 / bf16x3 (k <= 32) or bf16x2 / bf16x2_bf16 (k <= 8, one window), one hidden "
+                  "layer, no BN, "
                   "stride 1");
   VISSM_CHECK_ARG(w && u && C && theta_term && theta && obs && obs_bin && x && logsig && du && dC && dtheta_term && gr,
                   "flow_ar_elbo_fused: null pointer");

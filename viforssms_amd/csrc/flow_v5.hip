@@ -100,6 +100,13 @@ __device__ __forceinline__ f4 mm(const Fr4<NP>& a, const Fr4<NP>& b, f4 c) {
   }
   return mfma16(a.h, b.h, c);
 }
+// K = 16 product with the WEIGHT as the A operand: NP = 2 (split weights, bf16 activations) adds a_lo b_hi
+template <int NP>
+__device__ __forceinline__ f4 mm_w4(const Fr4<NP>& a, const Fr4<NP>& b, f4 c) {
+  if constexpr (NP >= 2) c = mfma16(a.l, b.h, c);
+  if constexpr (NP == 3) c = mfma16(a.h, b.l, c);
+  return mfma16(a.h, b.h, c);
+}
 // one operand exact in bf16 (ones / selections)
 template <int NP>
 __device__ __forceinline__ f4 mm_ax(bf8 a, const Fr8<NP>& b, f4 c) {
@@ -958,14 +965,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           wvh[rb] = whp[16 * rb + c];
-          if constexpr (NP == 3) wvl[rb] = whp[HP + 16 * rb + c];
+          if constexpr (NP >= 2) wvl[rb] = whp[HP + 16 * rb + c];
         }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           Fr4<NP> wa;
           wa.h = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
-          if constexpr (NP == 3) wa.l = __builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u});
-          D[rb] = mm<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
+          if constexpr (NP >= 2) wa.l = __builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u});
+          D[rb] = mm_w4<NP>(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[rb][r] = 4 * rb + r < NR ? D[rb][r] * elu_d(XN[rb][r]) : 0.f;
         }
@@ -1292,10 +1299,15 @@ __device__ __forceinline__ bf8 tr_frag2(const __bf16* img, int hb, int g, int c)
   return cat8(tr_read(img, hb, g, c), tr_read(img + P * HP, hb, g, c));
 }
 
-// NPR = 2 (fused variant only, VISSM_PREC_BF16X2): the forward recompute -- the values that reach the ELBO through
-// x and log sigma -- on split weights (w_hi u + w_lo u, the bf16x2 forward's products; lo planes of its 14 fragments
-// in LDS), the backward products bf16
-template <bool FZ, bool DU, bool TF, int NPR = 1>
+// NPR = 2: the forward recompute -- the values that reach the ELBO through x and log sigma, and every activation
+// the backward differentiates at -- on split weights (w_hi u + w_lo u, the bf16x2 forward's products; lo planes of
+// the recompute's fragments in LDS).  SB (split backward, needs NPR = 2; VISSM_PREC_BF16X2): the backward chain's
+// weight products too -- the head backward W~h (g_mu, g_r), dX = W~ dZ, dcon = w_eps dA0 -- as w_hi x + w_lo x; the
+// position contractions (dW, dW_eps, dW_head, d theta, dC: activation x gradient operands) stay single bf16
+// products, whose independent per-position roundings average out.  CPU emulation at the AR-cfg length
+// (scripts/bf16_grad_emul.py): gradient 2.5e-3 (bf16) / 2.2e-3 (bf16x2f: split forward only) -> 7e-5 with SB.
+// NPR = 2 without SB: the bf16x2f host mode's fused last flow (VISSM_PREC_BF16X2_BF16: backward products bf16).
+template <bool FZ, bool DU, bool TF, int NPR = 1, bool SB = false>
 __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __restrict__ u, const float* __restrict__ C,
                                                       const float* __restrict__ tht, const float* __restrict__ gout,
                                                       const float* __restrict__ dls, const bf8* __restrict__ img,
@@ -1303,29 +1315,41 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
                                                       float* __restrict__ dC_slab, float* __restrict__ dth_slab,
                                                       float* __restrict__ dW_slab, float* __restrict__ halo,
                                                       const u4* __restrict__ thf, FzArgs fz = FzArgs{}) {
+  static_assert(!SB || NPR == 2, "the split backward chain goes with the split recompute");
   constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
   constexpr int PO = FZ ? P - 1 : P;
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
+  constexpr int UWN = 48;       // u window entries: the layer-0 fragment reads up to c + 8 g + 7 <= 46
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW2][2][2 * P * HP];  // [wave][slot][row 16 cb + position][64 h]
   __shared__ float dthl[NW2][S][DTH];
   __shared__ __attribute__((aligned(16))) float dths[NW2][4];
   __shared__ float carry[NW2][S][KP2];
-  __shared__ float gsc[NW2][2][P];
-  __shared__ float uwin[NW2][2][64];
+  __shared__ float uwin[NW2][2][UWN];
+  // the upstream gradient g_mu at p (read by the head backward), then g_mu sigma (the du pass-through term)
   __shared__ float gwin[NW2][2][P];
   __shared__ float dscr[NW2][2][KP2][QW2];
   constexpr bool ZLS = FZ && NPR == 1;  // per-column log sigma sums in LDS
   __shared__ float zls[ZLS ? NW2 : 1][ZLS ? S : 1][P];
-  __shared__ bf8 slo[NPR == 2 ? 14 : 1][64];  // NPR = 2: lo planes of WF 0..7, WE 0..3, WH 0..1
+  // lo planes: NPR = 2 the recompute's WF 0..7 and WH 0..1 (slo[0..9]); SB the backward chain's WB 0..7 and WC 0..1
+  // (slo[RO..RO + 9]); the layer-0 WE 0..3 lo planes are nonzero in lane group 0 only (rows j < k <= 8; the theta
+  // fold's rows are exact bf16 splits): swe[ob][c]
+  constexpr int RO = NPR == 2 ? 10 : 0, NLO = RO + (SB ? 10 : 0);
+  __shared__ bf8 slo[NLO > 0 ? NLO : 1][64];
+  __shared__ bf8 swe[NPR == 2 ? 4 : 1][16];
   __shared__ float zcar[FZ ? NW2 : 1][FZ ? S : 1];
-  if constexpr (NPR == 2) {  // the image holds [frag][hi, lo][lane]: hi planes to sh, the recompute's lo planes to slo
+  if constexpr (NPR == 2) {  // the image holds [frag][hi, lo][lane]: hi planes to sh, the lo planes to slo / swe
     constexpr int NFR = Shared<NH, KB, JB, NP>::NFR;
     for (int i = threadIdx.x; i < NFR * 64; i += NT2) sh.img[i >> 6][0][i & 63] = img[((i >> 6) * 2) * 64 + (i & 63)];
-    for (int i = threadIdx.x; i < 14 * 64; i += NT2) {
-      const int j = i >> 6, f = j < 8 ? j : (j < 12 ? 16 * NH + (j - 8) : 16 * NH + 4 * KB + 2 * JB + (j - 12));
+    for (int i = threadIdx.x; i < NLO * 64; i += NT2) {
+      const int j = i >> 6;
+      const int f = j < 8 ? j                                            // WF
+                  : j < 10 ? 16 * NH + 4 * KB + 2 * JB + (j - 8)         // WH
+                  : j < 18 ? 8 * NH + (j - 10)                           // WB
+                           : 16 * NH + 4 * KB + (j - 18);                // WC
       slo[j][i & 63] = img[(f * 2 + 1) * 64 + (i & 63)];
     }
+    for (int i = threadIdx.x; i < 4 * 16; i += NT2) swe[i >> 4][i & 15] = img[((16 * NH + (i >> 4)) * 2 + 1) * 64 + (i & 15)];
     for (int i = threadIdx.x; i < Shared<NH, KB, JB, NP>::NCST; i += NT2) sh.cst[i] = cst[i];
   } else {
     load_shared<NH, KB, JB, NP, NT2>(sh, img, cst);
@@ -1427,7 +1451,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          uwin[w][cb][lane] = uv[cb];
+          if (lane < UWN) uwin[w][cb][lane] = uv[cb];
           if (lane < P) gwin[w][cb][lane] = gv[cb];
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) X[cb][rb] = TF ? cr[rb] : cr[rb] + tr[cb][rb];
@@ -1453,10 +1477,15 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
           const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
+          bf8 wel = {};
+          if constexpr (NPR == 2) {
+            const bf8 v = swe[ob][c];
+            if (g == 0) wel = v;
+          }
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             acc[cb][ob] = X[cb][ob];
-            if constexpr (NPR == 2) acc[cb][ob] = mfma32(slo[8 + ob][lane], uf[cb].h, acc[cb][ob]);
+            if constexpr (NPR == 2) acc[cb][ob] = mfma32(wel, uf[cb].h, acc[cb][ob]);
             acc[cb][ob] = mm<NP>(wf, uf[cb], acc[cb][ob]);
           }
         }
@@ -1510,7 +1539,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             const Fr8<NP> xk = chain_frag<NP>(X[cb], ks);
-            if constexpr (NPR == 2) d[cb] = mfma32(slo[12 + ks][lane], xk.h, d[cb]);
+            if constexpr (NPR == 2) d[cb] = mfma32(slo[8 + ks][lane], xk.h, d[cb]);
             d[cb] = mm<NP>(wf, xk, d[cb]);
           }
         }
@@ -1545,7 +1574,6 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
           const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : 0.f;
           if (g == 0) {
-            gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the rest of the unit reads
             if (pv && (cb == 0 || two)) {
               fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
               if constexpr (ZLS) zls[w][bl2][c] += lsg;
@@ -1563,7 +1591,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         float dsig = gmu[cb] * uwin[w][cb][c + a.k];
         if (pv && (cb == 0 || two) && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig[cb]);
         gr[cb] = dsig * sigmoid_fast(rr[cb]);
-        if (g == 0) gsc[w][cb][c] = sig[cb];
+        if (g == 0) gwin[w][cb][c] = gmu[cb] * sig[cb];  // (after the reads of g_mu above: LDS order within the wave)
         // the head gradient G = (g_mu, g_r) at p = c into the I_1 image's padding rows 53, 54 (register (3, 1),
         // (3, 2) of lane group 1; unit 49 in row 52 rewritten unchanged): dW_head = I_1 G^T then takes both
         // operands from this one image, before the dZ image overwrites its slot
@@ -1585,9 +1613,12 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       // dZ = (w~_mu g_mu + w~_r g_r) * elu'(I_1): one K = 16 MFMA per row block per sample
       f4 D[2][4];
       {
-        unsigned wvh[4];
+        unsigned wvh[4], wvl[4];
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) wvh[rb] = whp[16 * rb + c];
+        for (int rb = 0; rb < 4; ++rb) {
+          wvh[rb] = whp[16 * rb + c];
+          if constexpr (SB) wvl[rb] = whp[HP + 16 * rb + c];  // the lo plane of the (mu, r) pairs
+        }
         const bool g0 = g == 0;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1595,7 +1626,9 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) {
             const bf4 wa = __builtin_bit_cast(bf4, u2{g0 ? wvh[rb] : 0u, 0u});
-            D[cb][rb] = mfma16(wa, gf2, f4{0.f, 0.f, 0.f, 0.f});
+            f4 d0 = f4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (SB) d0 = mfma16(__builtin_bit_cast(bf4, u2{g0 ? wvl[rb] : 0u, 0u}), gf2, d0);
+            D[cb][rb] = mfma16(wa, gf2, d0);
           }
         }
         fence2<FZ>();
@@ -1623,7 +1656,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int ib = 0; ib < 4; ++ib) {
           const Fr8<NP> wb = wfrag(sh, 8 * NH + ib * 2 + ks, lane);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) dX[cb][ib] = mm<NP>(wb, df[cb], dX[cb][ib]);
+          for (int cb = 0; cb < 2; ++cb) {
+            if constexpr (SB) dX[cb][ib] = mfma32(slo[RO + ib * 2 + ks][lane], df[cb].h, dX[cb][ib]);
+            dX[cb][ib] = mm<NP>(wb, df[cb], dX[cb][ib]);
+          }
         }
       }
       fence2<FZ>();
@@ -1656,7 +1692,11 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int ks = 0; ks < 2; ++ks) {
           const Fr8<NP> wc = wfrag(sh, fwc + ks, lane);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) dcn[cb] = mm<NP>(wc, chain_frag<NP>(D[cb], ks), dcn[cb]);
+          for (int cb = 0; cb < 2; ++cb) {
+            const Fr8<NP> dk = chain_frag<NP>(D[cb], ks);
+            if constexpr (SB) dcn[cb] = mfma32(slo[RO + 8 + ks][lane], dk.h, dcn[cb]);
+            dcn[cb] = mm<NP>(wc, dk, dcn[cb]);
+          }
         }
       }
       if constexpr (FZ && !ZLS) {
@@ -1741,7 +1781,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             for (int j = 0; j + w2 < KP2; j += 2 * w2) t[j] += t[j + w2];
           float v = t[0];
           const int oq2 = q - a.k;
-          if (oq2 >= 0 && oq2 < nP) v += gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
+          if (oq2 >= 0 && oq2 < nP) v += gwin[w][cbq][oq2];  // g_mu sigma
           const int blq = cbq ? blv[1] : blv[0];
           if (q < a.k) v += carry[w][blq][q];
           if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.L + t0 + q] = v;
@@ -2552,7 +2592,8 @@ static int n_wgrad(const VissmFlowDesc* d) {
 
 static int jb_of(int k) { return (k + 15) / 16; }
 static int np_of(const VissmFlowDesc* d) {
-  return d->precision == VISSM_PREC_BF16X3 ? 3 : d->precision == VISSM_PREC_BF16X2 ? 2 : 1;
+  return d->precision == VISSM_PREC_BF16X3 ? 3
+       : (d->precision == VISSM_PREC_BF16X2 || d->precision == VISSM_PREC_BF16X2_BF16) ? 2 : 1;
 }
 
 struct Ws {
@@ -2607,7 +2648,7 @@ static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
-  a.dc16 = (d->n_win == 1 && (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2)) ? 1 : 0;
+  a.dc16 = (d->n_win == 1 && d->precision != VISSM_PREC_FP32 && d->precision != VISSM_PREC_BF16X3) ? 1 : 0;
   a.ncu = device_cus();
   return a;
 }
@@ -2660,9 +2701,9 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowPar
   }
 }
 
-// the two-sample backward covers the AR configurations' flow shape
+// the two-sample backward covers the AR configurations' flow shape, at bf16 and bf16x2 (split weights: SB)
 static bool bwd2_ok(const VissmFlowDesc* d, const Geom& g) {
-  return d->precision == VISSM_PREC_BF16 && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
+  return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X2) && d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out &&
          d->k <= KP2 && d->H <= kMaxH && d->n_win == 1 && g.S == S;
 }
 
@@ -2693,7 +2734,7 @@ bool VISSM_FLOW5_API(flow5_supports)(const VissmFlowDesc* d) {
   if (d->H > kMaxH || d->k > 64) return false;
   if (d->precision == VISSM_PREC_BF16) return d->n_hidden == 1 || d->n_hidden == 3;
   if (d->precision == VISSM_PREC_BF16X3) return d->n_hidden == 1 && d->k <= 32;
-  if (d->precision == VISSM_PREC_BF16X2) return d->n_hidden == 1 && d->k <= 32;  // forward kernel only
+  if (d->precision == VISSM_PREC_BF16X2) return d->n_hidden == 1 && d->k <= 32;
   return false;
 }
 
@@ -2714,6 +2755,9 @@ void VISSM_FLOW5_API(flow5_geometry)(const VissmFlowDesc* d, int which, int32_t*
     if (NP == 3) {                                                                                 \
       if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 3>), __VA_ARGS__);                           \
       else hipLaunchKernelGGL((KERNEL<1, 1, 2, 3>), __VA_ARGS__);                                   \
+    } else if (NP == 2) {                                                                          \
+      if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 2>), __VA_ARGS__);                           \
+      else hipLaunchKernelGGL((KERNEL<1, 1, 2, 2>), __VA_ARGS__);                                   \
     } else if (NHd == 1) {                                                                         \
       switch (JB) {                                                                                \
         case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 1>), __VA_ARGS__); break;                       \
@@ -2738,6 +2782,9 @@ void VISSM_FLOW5_API(flow5_geometry)(const VissmFlowDesc* d, int which, int32_t*
     if (NP == 3) {                                                                                 \
       if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 3, TAIL>), __VA_ARGS__);                           \
       else hipLaunchKernelGGL((KERNEL<1, 1, 2, 3, TAIL>), __VA_ARGS__);                                   \
+    } else if (NP == 2) {                                                                          \
+      if (JB == 1) hipLaunchKernelGGL((KERNEL<1, 1, 1, 2, TAIL>), __VA_ARGS__);                           \
+      else hipLaunchKernelGGL((KERNEL<1, 1, 2, 2, TAIL>), __VA_ARGS__);                                   \
     } else if (NHd == 1) {                                                                         \
       switch (JB) {                                                                                \
         case 1: hipLaunchKernelGGL((KERNEL<1, 1, 1, 1, TAIL>), __VA_ARGS__); break;                       \
@@ -2863,11 +2910,16 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
 #undef BWD2N_LAUNCH
   } else if (b2) {
     const dim3 grid2((g.n_items + NW2 - 1) / NW2);
-#define BWD2_LAUNCH(DU_, TF_)                                                                                     \
-  hipLaunchKernelGGL((bwd2_kernel<false, DU_, TF_>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, dlogsig, \
-                     ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, FzArgs{})
-    if (du) { if (fold) BWD2_LAUNCH(true, true); else BWD2_LAUNCH(true, false); }
-    else { if (fold) BWD2_LAUNCH(false, true); else BWD2_LAUNCH(false, false); }
+#define BWD2_LAUNCH(DU_, TF_, NPR_, SB_)                                                                          \
+  hipLaunchKernelGGL((bwd2_kernel<false, DU_, TF_, NPR_, SB_>), grid2, dim3(NT2), 0, st, a, u, ws.Cp, ws.thp, du_next, \
+                     dlogsig, ws.img, ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, FzArgs{})
+    if (np_of(d) == 2) {  // bf16x2: split-weight recompute and backward chain
+      if (du) { if (fold) BWD2_LAUNCH(true, true, 2, true); else BWD2_LAUNCH(true, false, 2, true); }
+      else { if (fold) BWD2_LAUNCH(false, true, 2, true); else BWD2_LAUNCH(false, false, 2, true); }
+    } else {
+      if (du) { if (fold) BWD2_LAUNCH(true, true, 1, false); else BWD2_LAUNCH(true, false, 1, false); }
+      else { if (fold) BWD2_LAUNCH(false, true, 1, false); else BWD2_LAUNCH(false, false, 1, false); }
+    }
 #undef BWD2_LAUNCH
   } else if (du)
     FLOW5_DISPATCH_T(bwd_kernel, false COMMA true, d->n_hidden, jb_of(d->k), np_of(d), grid, dim3(NT), 0, st, a, u,
@@ -2907,7 +2959,7 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
 bool VISSM_FLOW5_API(flow5_ar_fused_supports)(const VissmFlowDesc* d) {
   const bool shape = d->n_hidden == 1 && !d->bn && !d->stride2 && !d->swap_out && d->k <= 32 && d->H <= kMaxH &&
                      d->n_win >= 1;
-  if (d->precision == VISSM_PREC_BF16X2)  // split-weight recompute: the two-sample kernel's shape only
+  if (d->precision == VISSM_PREC_BF16X2 || d->precision == VISSM_PREC_BF16X2_BF16)  // the two-sample kernel's shape only
     return shape && d->k <= KP2 && d->n_win == 1;
   return (d->precision == VISSM_PREC_BF16 || d->precision == VISSM_PREC_BF16X3) && shape;
 }
@@ -2937,7 +2989,9 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
                   "flow_ar_elbo_fused: workspace too small");
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws, true);
-  const bool x2 = d->precision == VISSM_PREC_BF16X2;
+  // bf16x2: split-weight recompute and backward chain; bf16x2_bf16: split-weight recompute, bf16 backward products
+  const bool x2 = d->precision == VISSM_PREC_BF16X2 || d->precision == VISSM_PREC_BF16X2_BF16;
+  const bool sb = d->precision == VISSM_PREC_BF16X2;
   // bf16x2 has only the two-sample kernel: it must meet that kernel's geometry (bwd2_ok minus the precision test)
   VISSM_CHECK_ARG(!x2 || (g.S == S && d->n_win == 1 && d->k <= KP2),
                   "flow_ar_elbo_fused: bf16x2 needs the two-sample kernel's geometry (one window, k <= %d)", KP2);
@@ -2959,12 +3013,13 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   prof_begin(VISSM_PROF_FLOW_BWD, st);
   prof_begin(VISSM_PROF_FLOW_FUSED, st);
   if (b2) {
-#define BWD2F_LAUNCH(TF_, NPR_)                                                                                      \
-  hipLaunchKernelGGL((bwd2_kernel<true, true, TF_, NPR_>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u,   \
+#define BWD2F_LAUNCH(TF_, NPR_, SB_)                                                                                 \
+  hipLaunchKernelGGL((bwd2_kernel<true, true, TF_, NPR_, SB_>), dim3((g.n_items + NW2 - 1) / NW2), dim3(NT2), 0, st, a, u, \
                      ws.Cp, ws.thp, static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), ws.img,     \
                      ws.cst, du, ws.dC_slab, ws.dth_slab, ws.dW_slab, ws.halo, ws.thf, fz)
-    if (x2) { if (fold) BWD2F_LAUNCH(true, 2); else BWD2F_LAUNCH(false, 2); }
-    else { if (fold) BWD2F_LAUNCH(true, 1); else BWD2F_LAUNCH(false, 1); }
+    if (sb) { if (fold) BWD2F_LAUNCH(true, 2, true); else BWD2F_LAUNCH(false, 2, true); }
+    else if (x2) { if (fold) BWD2F_LAUNCH(true, 2, false); else BWD2F_LAUNCH(false, 2, false); }
+    else { if (fold) BWD2F_LAUNCH(true, 1, false); else BWD2F_LAUNCH(false, 1, false); }
 #undef BWD2F_LAUNCH
   } else
     FLOW5_FZ_DISPATCH(jb_of(d->k), np_of(d), dim3(g.blocks), dim3(NT), 0, st, a, u, ws.Cp, wn, ws.thp,

@@ -462,8 +462,9 @@ class Engine:
         fl = self.flows[-1]
         L = md.kernel_ext - (md.n_flows - 1) * md.k
         # bf16x2f: the fused kernel recomputes the flow on split weights (the bf16x2 forward's products: x and log
-        # sigma at that precision) and runs its backward products at bf16 (VISSM_PREC_BF16X2 on the fused entry)
-        prec = _lib.VISSM_PREC_BF16X2 if self.precision == _lib.VISSM_PREC_BF16X2F else self.precision
+        # sigma at that precision) and runs its backward products at bf16 (VISSM_PREC_BF16X2_BF16); bf16x2 runs
+        # every weight product split (VISSM_PREC_BF16X2)
+        prec = _lib.VISSM_PREC_BF16X2_BF16 if self.precision == _lib.VISSM_PREC_BF16X2F else self.precision
         return FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
                          swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=prec,
                          chunk_tiles=self.chunk_tiles)
