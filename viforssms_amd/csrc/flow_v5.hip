@@ -184,6 +184,17 @@ __device__ __forceinline__ float elu_fast(float x) {
   if constexpr (MED3) return __builtin_amdgcn_fmed3f(x, en, 0.f);
   return x > 0.f ? x : en;
 }
+// elu_fast<true> of a register's four rows, the four v_exp_f32 issued before their first use (one at a time, the
+// result of each transcendental is consumed by the next instruction and costs an s_nop wait state)
+__device__ __forceinline__ f4 elu4(const f4& x, int nvalid) {
+  f4 e, y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) e[r] = __builtin_amdgcn_exp2f(x[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    y[r] = r < nvalid ? __builtin_amdgcn_fmed3f(x[r], __builtin_fmaf(kLog2e, e[r], -kLog2e), 0.f) : 0.f;
+  return y;
+}
 // (min(y', 0) as a median: fminf would add a NaN-canonicalising v_max per element)
 __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
@@ -1493,8 +1504,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
         fence2<FZ>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1525,8 +1535,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
         fence2<FZ>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -2003,8 +2012,7 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+          X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
 #pragma unroll
       for (int l = 0; l < NH; ++l) {
 #pragma unroll
@@ -2027,8 +2035,7 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
       }
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
@@ -2210,8 +2217,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
           fence();
@@ -2237,10 +2243,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            for (int rb = 0; rb < 4; ++rb) X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
         }
         fence();
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
