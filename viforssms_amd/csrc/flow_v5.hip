@@ -184,17 +184,6 @@ __device__ __forceinline__ float elu_fast(float x) {
   if constexpr (MED3) return __builtin_amdgcn_fmed3f(x, en, 0.f);
   return x > 0.f ? x : en;
 }
-// elu_fast<true> of a register's four rows, the four v_exp_f32 issued before their first use (one at a time, the
-// result of each transcendental is consumed by the next instruction and costs an s_nop wait state)
-__device__ __forceinline__ f4 elu4(const f4& x, int nvalid) {
-  f4 e, y;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) e[r] = __builtin_amdgcn_exp2f(x[r]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    y[r] = r < nvalid ? __builtin_amdgcn_fmed3f(x[r], __builtin_fmaf(kLog2e, e[r], -kLog2e), 0.f) : 0.f;
-  return y;
-}
 // (min(y', 0) as a median: fminf would add a NaN-canonicalising v_max per element)
 __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
@@ -1330,15 +1319,19 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
   constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
   constexpr int PO = FZ ? P - 1 : P;
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
-  constexpr int UWN = 48;       // u window entries: the layer-0 fragment reads up to c + 8 g + 7 <= 46
+  // u window entries: the layer-0 fragment reads up to c + 8 g + 7 <= 46 (48 in the split-weight variants, whose
+  // lo planes need the LDS; 64 otherwise: an unmasked store, the measured bf16 code)
+  constexpr int UWN = NPR == 2 ? 48 : 64;
   __shared__ Shared<NH, KB, JB, NP> sh;
   __shared__ __bf16 timg[NW2][2][2 * P * HP];  // [wave][slot][row 16 cb + position][64 h]
   __shared__ float dthl[NW2][S][DTH];
   __shared__ __attribute__((aligned(16))) float dths[NW2][4];
   __shared__ float carry[NW2][S][KP2];
   __shared__ float uwin[NW2][2][UWN];
-  // the upstream gradient g_mu at p (read by the head backward), then g_mu sigma (the du pass-through term)
+  // the upstream gradient g_mu at p (read by the head backward); NPR = 2 (LDS for the lo planes): then overwritten
+  // with g_mu sigma, the du pass-through term, instead of keeping sigma in gsc
   __shared__ float gwin[NW2][2][P];
+  __shared__ float gsc[NPR == 2 ? 1 : NW2][2][P];
   __shared__ float dscr[NW2][2][KP2][QW2];
   constexpr bool ZLS = FZ && NPR == 1;  // per-column log sigma sums in LDS
   __shared__ float zls[ZLS ? NW2 : 1][ZLS ? S : 1][P];
@@ -1462,7 +1455,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          if (lane < UWN) uwin[w][cb][lane] = uv[cb];
+          if (UWN == 64 || lane < UWN) uwin[w][cb][lane] = uv[cb];
           if (lane < P) gwin[w][cb][lane] = gv[cb];
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) X[cb][rb] = TF ? cr[rb] : cr[rb] + tr[cb][rb];
@@ -1504,7 +1497,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         fence2<FZ>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1535,7 +1529,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         fence2<FZ>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -1583,6 +1578,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
           const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : 0.f;
           if (g == 0) {
+            if constexpr (NPR == 1) gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the du section reads
             if (pv && (cb == 0 || two)) {
               fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
               if constexpr (ZLS) zls[w][bl2][c] += lsg;
@@ -1600,7 +1596,13 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         float dsig = gmu[cb] * uwin[w][cb][c + a.k];
         if (pv && (cb == 0 || two) && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig[cb]);
         gr[cb] = dsig * sigmoid_fast(rr[cb]);
-        if (g == 0) gwin[w][cb][c] = gmu[cb] * sig[cb];  // (after the reads of g_mu above: LDS order within the wave)
+        if (g == 0) {
+          if constexpr (NPR == 2) {
+            if constexpr (DU) gwin[w][cb][c] = gmu[cb] * sig[cb];  // (after the reads of g_mu above: LDS order)
+          } else {
+            gsc[w][cb][c] = sig[cb];
+          }
+        }
         // the head gradient G = (g_mu, g_r) at p = c into the I_1 image's padding rows 53, 54 (register (3, 1),
         // (3, 2) of lane group 1; unit 49 in row 52 rewritten unchanged): dW_head = I_1 G^T then takes both
         // operands from this one image, before the dZ image overwrites its slot
@@ -1790,7 +1792,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             for (int j = 0; j + w2 < KP2; j += 2 * w2) t[j] += t[j + w2];
           float v = t[0];
           const int oq2 = q - a.k;
-          if (oq2 >= 0 && oq2 < nP) v += gwin[w][cbq][oq2];  // g_mu sigma
+          if (oq2 >= 0 && oq2 < nP) v += NPR == 2 ? gwin[w][cbq][oq2] : gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
           const int blq = cbq ? blv[1] : blv[0];
           if (q < a.k) v += carry[w][blq][q];
           if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.L + t0 + q] = v;
@@ -2012,7 +2014,8 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
-          X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
 #pragma unroll
       for (int l = 0; l < NH; ++l) {
 #pragma unroll
@@ -2035,7 +2038,8 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
       }
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
@@ -2217,7 +2221,8 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
-            X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
           fence();
@@ -2243,7 +2248,10 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb) X[cb][rb] = elu4(acc[cb][rb], NR - 4 * rb);
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
         }
         fence();
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
