@@ -154,21 +154,26 @@ def cpu_baseline(args, obs, ob, tt):
     B = min(args.cpu_B, args.B)
     host = host_cpu()
     default_threads = torch.get_num_threads()
+    host["cgroup_cpus"] = cgroup_cpus()
+    # nproc threads unless the cgroup grants fewer CPUs: on the GPU box nproc = 256 while the quota is 16, and 256
+    # threads on 16 CPUs ran one step in 134 s (2.4e3 transitions/s, profiles/r04/bench_full_r04b.json) -- an
+    # oversubscription artefact, not the host's rate
+    usable = host["nproc"] if not host["cgroup_cpus"] else min(host["nproc"], max(1, int(host["cgroup_cpus"])))
     lines = []
-    for threads in sorted({default_threads, host["nproc"]}):
+    for threads in sorted({default_threads, usable}):
         torch.set_num_threads(threads)
         secs = args.cpu_seconds if threads == default_threads else args.cpu_seconds / 2
         t, n, _ = _cpu_ar_step_rate(B, args.M, args.k, args.T, obs, ob, tt, secs, args.cpu_min_steps)
         lines.append({"threads": threads, "value": B * args.M / t, "s_per_step": t, "steps": n})
     torch.set_num_threads(default_threads)
     best = max(lines, key=lambda x: x["value"])
-    host["cgroup_cpus"] = cgroup_cpus()
     return {"value": best["value"], "unit": "transitions/s", "cores": best["threads"], "kind": "port", "host": host,
             "by_threads": lines,
             "sample": f"fp32 CPU restatement of the TF1 step (oracle/nma_oracle.py) on B={B} trajectories x "
                       f"M={args.M} (T={args.T}, k={args.k}), median of the steps after 2 warm-up, at "
                       f"{' and '.join(str(x['threads']) for x in lines)} torch threads (nproc = {host['nproc']}, "
-                      f"cgroup CPU quota = {host['cgroup_cpus']}); value = the faster ({best['threads']} threads, "
+                      f"cgroup CPU quota = {host['cgroup_cpus']}: threads capped at the quota); value = the faster "
+                      f"({best['threads']} threads, "
                       f"{best['s_per_step']:.2f} s/step)"}
 
 

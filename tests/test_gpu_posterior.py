@@ -64,10 +64,12 @@ def _post_stats(theta):
 TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance at step 0, after)
     "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4, 1e-4),
     "bf16x2f": (20, 5000, 8, 5000, 0.0, 5e-3, 1e-4, 5e-3),
-    # bf16x2 (split weights in the backward chain too: gradient within 1e-3): the fp32 case's bar on the posterior
-    # (measured 3.5e-6 over the first 4 steps against a 2e-5 floor); the ELBO within 1e-4 at the first step and 1e-3
-    # after (the steps' parameters differ by the gradient's ~7e-5 relative error: 1.5e-4 measured at step 3)
-    "bf16x2": (20, 5000, 8, 5000, 10.0, 2e-5, 1e-4, 1e-3),
+    # bf16x2 (split weights in the backward chain too: gradient within 1e-3).  Measured (profiles/r04/
+    # pytest_posterior_bf16x2.log): the posterior stays within the fp32 case's bar (10x the float32 oracle's drift +
+    # 2e-5) for 16 steps (<= 1.6e-5), then drifts to 8.9e-5 by step 20 -- Adamax's normalised steps pass the
+    # gradient's ~1e-4 relative error (bf16 gradient operands) into the parameters; the ELBO 2.3e-5 at the first step,
+    # <= 9.3e-4 after.  Held to 10x the float32 drift + 1.5e-4 and ELBO 1e-4 / 2e-3.  (bf16: 2.9e-3 and 1.4e-2.)
+    "bf16x2": (20, 5000, 8, 5000, 10.0, 1.5e-4, 1e-4, 2e-3),
     # bf16, the headline precision: measured over 20 steps (profiles/r04/pytest_gpu_full_first.log) posterior mean / sd
     # 2.9e-3 / 2.5e-3 from the float64 trajectory (growing ~linearly: Adamax passes the bf16 gradients' rounding into
     # every step), ELBO 1.1e-3 at the first step, 1.4e-2 worst after; held to 5e-3, 5e-3 and 2e-2
