@@ -1,9 +1,10 @@
 #!/bin/bash
-# A/B of the full AR-cfg training step over the library builds in abl/*.so (alternating, ROUNDS rounds):
+# A/B of the full AR-cfg training step over the library builds given as arguments (default abl/*.so; alternating,
+# ROUNDS rounds):
 # ms per step, backward per launch (average and per variant), roofline fraction.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
-for r in $(seq 1 ${ROUNDS:-2}); do for L in abl/*.so; do
+for r in $(seq 1 ${ROUNDS:-2}); do for L in ${@:-abl/*.so}; do
   n=$(basename $L .so)
   VISSM_LIB=$ROOT/$L timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 2 --cpu-baseline off \
     --parity-line off --families off $EXTRA > "$OUT/ab_$n.json" 2>"$OUT/ab_$n.err" || { tail -5 "$OUT/ab_$n.err"; exit 4; }
