@@ -269,6 +269,44 @@ int vissm_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, v
 int vissm_split_bf16(const float* x, void* hi, void* lo, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Window-shared feature branch + the first conv's feature channels (AR.py:53-62;
+ * SV_dense.py:53-62; fitz_nag_NVP.py:71-79): per window w,
+ *   F = elu(elu(elu(elu(h0 W0 + b0) W1 + b1) W2 + b2) W3 + b3)        [Lf][H]
+ *   C[w][m][o] = conv_b[o] + sum_{j<k} sum_{i<H} F[s m + j][i] conv_w[j][1 + i][o],  m < Lh
+ * (the sample channel conv_w[j][0][:] is the flow kernel's w_eps).  h0: the window's
+ * time-feature rows, Lf rows of Cin floats, windows in_win_stride floats apart.
+ * fwd writes C [n_win][Lh][H] and the four layer outputs act [4][n_win][Lf][H] (rows
+ * s (Lh - 1) + k .. Lf - 1 unused); bwd takes dC and writes (not accumulates) the
+ * gradients of W0..W3, b0..b3, conv_w (its sample channel 0) and conv_b.
+ * Replaces the four tf.layers.dense and the feature part of tf.layers.conv1d with
+ * their gradients.  Cin <= 63, H <= 64, k <= 64, stride 1 | 2; deterministic.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t n_win, Lf, Cin, H, k, stride, Lh;
+  int64_t in_win_stride;
+} VissmFeatDesc;
+
+typedef struct {
+  const float* w[4];    /* W0 [Cin][H], W1..W3 [H][H] */
+  const float* b[4];    /* [H] */
+  const float* conv_w;  /* [k][1 + H][H] */
+  const float* conv_b;  /* [H] */
+} VissmFeatParams;
+
+typedef struct {
+  float* w[4];
+  float* b[4];
+  float* conv_w;
+  float* conv_b;
+} VissmFeatGrads;
+
+size_t vissm_feat_workspace_size(const VissmFeatDesc* d);
+int vissm_feat_fwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float* h0, float* C, float* act,
+                   void* stream);
+int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float* h0, const float* act,
+                   const float* dC, const VissmFeatGrads* g, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;
  * lotka_volterra_partial.py:366-386; SV_dense.py:304-328) from device-resident
  * padded channel tables (built once, AR.py:135-150), keyed by the step's window

@@ -213,3 +213,15 @@ def test_abi_struct_layouts_match_ctypes():
         f(which, out)
         assert out[0] == ctypes.sizeof(cls), (cls.__name__, out[0], ctypes.sizeof(cls))
         assert out[1] == getattr(cls, last).offset, (cls.__name__, last)
+
+
+def test_feat_workspace_size_validates_without_gpu():
+    """vissm_feat_workspace_size (host arithmetic): the fused feature branch's shape limits (Cin <= 63, H <= 64,
+    k <= 64, stride 1 | 2, s (Lh - 1) + k <= Lf) are checked before any launch; 0 = rejected."""
+    from viforssms_amd import _lib
+    lib = _lib.load()
+    ok = _lib.FeatDesc(1, 5024, 14, 50, 8, 1, 5017, 5024 * 14)
+    assert lib.vissm_feat_workspace_size(ctypes.byref(ok)) > 0
+    for bad in [(1, 5024, 14, 65, 8, 1, 5017, 0), (1, 5024, 64, 50, 8, 1, 5017, 0), (1, 5024, 14, 50, 65, 1, 4960, 0),
+                (1, 5024, 14, 50, 8, 3, 1000, 0), (1, 5024, 14, 50, 8, 1, 5018, 0), (2, 100, 14, 50, 8, 1, 93, 99 * 14)]:
+        assert lib.vissm_feat_workspace_size(ctypes.byref(_lib.FeatDesc(*bad))) == 0, bad

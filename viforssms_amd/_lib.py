@@ -62,6 +62,18 @@ class GatherDesc(ctypes.Structure):
                 ("c_pitch", _i64), ("os_r", _i64), ("os_j", _i64), ("os_c", _i64)]
 
 
+class FeatDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("n_win", "Lf", "Cin", "H", "k", "stride", "Lh")] + [("in_win_stride", _i64)]
+
+
+class FeatParams(ctypes.Structure):
+    _fields_ = [("w", _c_void_p * 4), ("b", _c_void_p * 4), ("conv_w", _c_void_p), ("conv_b", _c_void_p)]
+
+
+class FeatGrads(ctypes.Structure):
+    _fields_ = [("w", _c_void_p * 4), ("b", _c_void_p * 4), ("conv_w", _c_void_p), ("conv_b", _c_void_p)]
+
+
 THETA_MAX_P, THETA_MAX_BIJ = 5, 8
 
 
@@ -94,6 +106,11 @@ SIGNATURES = {
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _f32,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         ctypes.POINTER(FlowGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_feat_workspace_size": (_size_t, [ctypes.POINTER(FeatDesc)]),
+    "vissm_feat_fwd": (_i32, [ctypes.POINTER(FeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p, _c_void_p,
+                              _c_void_p]),
+    "vissm_feat_bwd": (_i32, [ctypes.POINTER(FeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p, _c_void_p,
+                              ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
     "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,

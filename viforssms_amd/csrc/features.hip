@@ -1,0 +1,478 @@
+// The window-shared feature branch of a flow and the first conv's feature channels, fused
+// (vissm_feat_fwd / vissm_feat_bwd).
+//
+// Reference: AR.py:53-62 (SV_dense.py:53-62, fitz_nag_NVP.py:71-79) -- four tf.layers.dense with ELU over the
+// window's time features, then the conv1d over [eps, features] (kernel [k][1 + H][H], bias, stride 1 or 2);
+// this computes the feature channels' part of that conv,
+//   C[w][m][o] = conv_b[o] + sum_{j < k} sum_{i < H} F[w][s m + j][i] conv_w[j][1 + i][o],
+//   F = elu(elu(elu(elu(h0 W0 + b0) W1 + b1) W2 + b2) W3 + b3),
+// which every sample of a window shares (the sample channel, conv_w[j][0][o] eps, is the flow kernel's).
+// These products are tiny ([~5000 x 50] x [50 x 50] per layer) and run as ~40 library / elementwise launches per
+// flow in torch; here one block computes a tile of kT output positions from its rows of F (recomputing the k - s
+// halo rows its neighbour also computes) with the weights staged in LDS, fp32 FMAs throughout.  The backward
+// partitions F's rows the same way: the transposed conv (dF), the conv's weight gradient over the tile's
+// positions, the MLP backward; per-block weight-gradient partials go to a slab summed in a fixed order
+// (deterministic; no atomics).
+#include "common.hpp"
+
+namespace vissm {
+namespace feat {
+
+constexpr int kT = 32;     // output positions per block (forward) / per m-range of a block (backward)
+constexpr int kNT = 256;   // 4 waves: lane = output unit, wave = row group
+constexpr int kMaxH = 64, kMaxCin = 63, kMaxK = 64;
+
+struct Args {
+  int n_win, Lf, Cin, H, k, s, Lh, Lu;   // Lu = s (Lh - 1) + k: the rows of F any output reads
+  int64_t in_ws;                         // floats between windows of h0 (rows of Cin floats)
+};
+
+struct Params {
+  const float* w[4];
+  const float* b[4];
+  const float* cw;   // conv kernel [k][1 + H][H]
+  const float* cb;
+};
+
+__device__ __forceinline__ float elu(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_d_out(float y) { return y > 0.f ? 1.f : y + 1.f; }  // from the output
+
+// weights [nin][H] (row pitch H in global) into LDS with row pitch wp
+__device__ __forceinline__ void stage_w(float* Ws, int wp, const float* g, int nin, int H) {
+  for (int idx = threadIdx.x; idx < nin * H; idx += kNT) Ws[(idx / H) * wp + idx % H] = g[idx];
+}
+// the feature channels of conv tap j, [H in][H out], with row pitch wp
+__device__ __forceinline__ void stage_tap(float* Ws, int wp, const float* cw, int j, int H) {
+  const float* g = cw + static_cast<size_t>(j) * (1 + H) * H + H;
+  for (int idx = threadIdx.x; idx < H * H; idx += kNT) Ws[(idx / H) * wp + idx % H] = g[idx];
+}
+
+// out[r][o] = elu(b[o] + sum_i in[r][i] W[i][o]) for r < R (rows in eight-row groups: rows up to the next
+// multiple of 32 are read, the buffers hold them); rows r < n_store also go to gout (row pitch H)
+__device__ void dense_elu(const float* in, int ip, int nin, const float* Ws, int wp, const float* bg, float* out,
+                          int op, int R, int H, float* gout, int n_store) {
+  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  if (o >= H) return;
+  const float bo = bg[o];
+  for (int r0 = rg * 8; r0 < R; r0 += 32) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = bo;
+    for (int i = 0; i < nin; ++i) {
+      const float wv = Ws[i * wp + o];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = fmaf(in[(r0 + q) * ip + i], wv, acc[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = r0 + q;
+      if (r < R) {
+        const float y = elu(acc[q]);
+        out[r * op + o] = y;
+        if (r < n_store) gout[static_cast<size_t>(r) * H + o] = y;
+      }
+    }
+  }
+}
+
+// LDS layout (floats) shared by both kernels: rows padded to the next multiple of 32
+__host__ __device__ inline int rows_pad(int r) { return (r + 31) / 32 * 32; }
+
+// forward: grid (ceil(Lh / kT), n_win)
+__global__ __launch_bounds__(kNT) void feat_fwd_kernel(Args a, Params p, const float* __restrict__ h0,
+                                                       float* __restrict__ C, float* __restrict__ act) {
+  extern __shared__ float sm[];
+  const int H = a.H, hp = H + 1, ip = a.Cin + 1;
+  const int w = blockIdx.y, m0 = blockIdx.x * kT;
+  const int nm = min(kT, a.Lh - m0);
+  const int r0 = a.s * m0;                                   // first row of F this block computes
+  const int R = min(a.s * (kT - 1) + a.k, a.Lu - r0);        // rows it computes
+  const bool last = m0 + kT >= a.Lh;
+  const int n_own = last ? R : min(a.s * kT, R);              // rows it stores (the next block recomputes the rest)
+  const int RP = rows_pad(a.s * (kT - 1) + a.k);
+  float* hA = sm;                                // [RP][max(Cin, H) + 1]
+  float* hB = hA + RP * max(ip, hp);             // [RP][H + 1]
+  float* Ws = hB + RP * hp;                      // [max(Cin, H)][H + 1]
+  const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
+  for (int idx = threadIdx.x; idx < RP * a.Cin; idx += kNT) {
+    const int r = idx / a.Cin, c = idx % a.Cin;
+    hA[r * ip + c] = r < R ? src[idx] : 0.f;
+  }
+  for (int idx = threadIdx.x; idx < RP * hp; idx += kNT) hB[idx] = 0.f;
+  stage_w(Ws, hp, p.w[0], a.Cin, H);
+  __syncthreads();
+  const size_t plane = static_cast<size_t>(a.n_win) * a.Lf * H;
+  float* ab = act + (static_cast<size_t>(w) * a.Lf + r0) * H;
+  dense_elu(hA, ip, a.Cin, Ws, hp, p.b[0], hB, hp, R, H, ab, n_own);
+  __syncthreads();
+  stage_w(Ws, hp, p.w[1], H, H);
+  __syncthreads();
+  dense_elu(hB, hp, H, Ws, hp, p.b[1], hA, hp, R, H, ab + plane, n_own);
+  __syncthreads();
+  stage_w(Ws, hp, p.w[2], H, H);
+  __syncthreads();
+  dense_elu(hA, hp, H, Ws, hp, p.b[2], hB, hp, R, H, ab + 2 * plane, n_own);
+  __syncthreads();
+  stage_w(Ws, hp, p.w[3], H, H);
+  __syncthreads();
+  dense_elu(hB, hp, H, Ws, hp, p.b[3], hA, hp, R, H, ab + 3 * plane, n_own);   // F in hA (pitch hp)
+  // rows of hA at and past R hold the previous layer's values: zero them (the conv reads up to RP rows)
+  for (int idx = threadIdx.x; idx < (RP - R) * hp; idx += kNT) hA[R * hp + idx] = 0.f;
+  // the conv over the feature channels: thread (o, rg) owns output rows rg*8 .. rg*8 + 7
+  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  for (int j = 0; j < a.k; ++j) {
+    __syncthreads();
+    stage_tap(Ws, hp, p.cw, j, H);
+    __syncthreads();
+    if (o < H) {
+      const float* Fr = hA + (a.s * rg * 8 + j) * hp;
+      for (int i = 0; i < H; ++i) {
+        const float wv = Ws[i * hp + o];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = fmaf(Fr[a.s * q * hp + i], wv, acc[q]);
+      }
+    }
+  }
+  if (o < H) {
+    const float bo = p.cb[o];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int m = rg * 8 + q;
+      if (m < nm) C[(static_cast<size_t>(w) * a.Lh + m0 + m) * H + o] = acc[q] + bo;
+    }
+  }
+}
+
+// gradient slab row layout: W0 [Cin][H], b0, W1, b1, W2, b2, W3, b3 ([H][H], [H]), conv taps [k][H][H], conv b [H]
+struct Off {
+  int w[4], b[4], cw, cb, n;
+};
+__host__ __device__ inline Off offsets(int Cin, int H, int k) {
+  Off f;
+  int o = 0;
+  for (int l = 0; l < 4; ++l) {
+    f.w[l] = o;
+    o += (l == 0 ? Cin : H) * H;
+    f.b[l] = o;
+    o += H;
+  }
+  f.cw = o;
+  o += k * H * H;
+  f.cb = o;
+  o += H;
+  f.n = o;
+  return f;
+}
+
+// part[i][o] = sum_{r < nr} X[r][i] G[r][o] for i < nin (thread (o, ig): i = ig, ig + 4, ...); written to slab
+__device__ void wgrad(const float* X, int xp, int nin, const float* G, int gp, int nr, int H, float* out) {
+  const int o = threadIdx.x & 63, ig = threadIdx.x >> 6;
+  if (o >= H) return;
+  for (int i0 = ig; i0 < nin; i0 += 64) {   // 16 inputs per pass: i0 + 4 t
+    float acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+    for (int r = 0; r < nr; ++r) {
+      const float g = G[r * gp + o];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[t] = fmaf(X[r * xp + min(i0 + 4 * t, nin - 1)], g, acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      if (i0 + 4 * t < nin) out[(i0 + 4 * t) * H + o] = acc[t];
+  }
+}
+
+// backward: grid (ceil(Lu / (s kT)), n_win); block b owns F rows [b s kT, (b + 1) s kT) and positions
+// m in [b kT, (b + 1) kT)
+__global__ __launch_bounds__(kNT) void feat_bwd_kernel(Args a, Params p, const float* __restrict__ h0,
+                                                       const float* __restrict__ act, const float* __restrict__ dC,
+                                                       float* __restrict__ slab) {
+  extern __shared__ float sm[];
+  const int H = a.H, hp = H + 1, ip = a.Cin + 1, k = a.k, s = a.s;
+  const int w = blockIdx.y, b = blockIdx.x;
+  const int TR = s * kT;
+  const int r0 = b * TR, nr = min(TR, a.Lu - r0);            // own rows of F
+  const int m0 = b * kT, nm = max(0, min(kT, a.Lh - m0));    // own positions
+  const int m_lo = r0 - (k - 1) >= 0 ? (r0 - (k - 1)) / s : -((k - 1 - r0 + s - 1) / s);  // floor((r0-k+1)/s)
+  const int nd = m0 + kT - m_lo;                              // staged dC rows [m_lo, m0 + kT)
+  const int RF = s * (kT - 1) + k;                            // staged F rows [r0, r0 + RF) for the conv gradient
+  const int DP = rows_pad(nd), FP = rows_pad(RF), GP = rows_pad(TR);
+  float* dCs = sm;                      // [DP][hp]
+  float* Fs = dCs + DP * hp;            // [FP][hp]
+  float* G0 = Fs + FP * hp;             // [GP][hp]  gradient rows (ping)
+  float* G1 = G0 + GP * hp;             // [GP][hp]  (pong)
+  float* Xs = G1 + GP * hp;             // [GP][max(ip, hp)]  a layer's input rows
+  float* Ws = Xs + GP * max(ip, hp);    // [max(Cin, H)][hp]
+  const size_t plane = static_cast<size_t>(a.n_win) * a.Lf * H;
+  const float* dCw = dC + static_cast<size_t>(w) * a.Lh * H;
+  for (int idx = threadIdx.x; idx < DP * hp; idx += kNT) {
+    const int r = idx / hp, c = idx % hp, m = m_lo + r;
+    dCs[idx] = (c < H && r < nd && m >= 0 && m < a.Lh) ? dCw[static_cast<size_t>(m) * H + c] : 0.f;
+  }
+  const float* F = act + 3 * plane + static_cast<size_t>(w) * a.Lf * H;
+  for (int idx = threadIdx.x; idx < FP * hp; idx += kNT) {
+    const int r = idx / hp, c = idx % hp, rr = r0 + r;
+    Fs[idx] = (c < H && r < RF && rr < a.Lu) ? F[static_cast<size_t>(rr) * H + c] : 0.f;
+  }
+  __syncthreads();
+  const Off of = offsets(a.Cin, H, k);
+  float* out = slab + (static_cast<size_t>(w) * gridDim.x + b) * of.n;
+  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  // conv bias: sum of the own positions' dC
+  if (rg == 0 && o < H) {
+    float sb = 0.f;
+    for (int m = 0; m < nm; ++m) sb += dCs[(m0 + m - m_lo) * hp + o];
+    out[of.cb + o] = sb;
+  }
+  // conv taps: dW_j[i][o] = sum_{own m} F[s m + j][i] dC[m][o] (F row s m + j - r0 = s (m - m0) + j)
+  if (o < H) {
+    for (int j = 0; j < k; ++j)
+      for (int i0 = rg; i0 < H; i0 += 64) {
+        float acc[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+        for (int m = 0; m < nm; ++m) {
+          const float g = dCs[(m0 + m - m_lo) * hp + o];
+          const float* Fr = Fs + (s * m + j) * hp;
+#pragma unroll
+          for (int t = 0; t < 16; ++t) acc[t] = fmaf(Fr[min(i0 + 4 * t, H - 1)], g, acc[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+          if (i0 + 4 * t < H) out[of.cw + (j * H + i0 + 4 * t) * H + o] = acc[t];
+      }
+  }
+  // dF[r][i] = sum_j sum_o dC[(r - j) / s][o] W_j[i][o] over (r - j) divisible by s: thread (i, rg) rows
+  // rg*8 .. rg*8 + 7 of each 32-row group
+  {
+    const int i = o;
+    for (int rb = 0; rb < TR; rb += 32) {
+      float acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+      for (int j = 0; j < k; ++j) {
+        __syncthreads();
+        stage_tap(Ws, hp, p.cw, j, H);
+        __syncthreads();
+        if (i < H) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int r = r0 + rb + rg * 8 + q - j;    // s m for the tap's position m
+            if (r % s != 0) continue;                    // wave-uniform (one row per wave and q)
+            const int mi = (r >= 0 ? r / s : -((-r + s - 1) / s)) - m_lo;
+            if (mi < 0 || mi >= nd) continue;
+            const float* dr = dCs + mi * hp;
+            float v = 0.f;
+            for (int oo = 0; oo < H; ++oo) v = fmaf(dr[oo], Ws[i * hp + oo], v);
+            acc[q] += v;
+          }
+        }
+      }
+      // dz4 = dF * elu'(F) (F from the staged rows: row r - r0 of Fs)
+      if (i < H) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int rl = rb + rg * 8 + q;
+          if (rl < GP) G0[rl * hp + i] = rl < nr ? acc[q] * elu_d_out(Fs[rl * hp + i]) : 0.f;
+        }
+      }
+    }
+  }
+  // the MLP backward, layer 3 down to 0: dW_l = X_l^T dz, db_l = sum dz, dz_prev = (dz W_l^T) * elu'(X_l)
+  float* Gc = G0;
+  float* Gn = G1;
+  for (int l = 3; l >= 0; --l) {
+    const int nin = l == 0 ? a.Cin : H, xp = l == 0 ? ip : hp;
+    __syncthreads();
+    if (l == 0) {
+      const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
+      for (int idx = threadIdx.x; idx < GP * a.Cin; idx += kNT) {
+        const int r = idx / a.Cin, c = idx % a.Cin;
+        Xs[r * ip + c] = r < nr ? src[idx] : 0.f;
+      }
+    } else {
+      const float* X = act + (l - 1) * plane + (static_cast<size_t>(w) * a.Lf + r0) * H;
+      for (int idx = threadIdx.x; idx < GP * hp; idx += kNT) {
+        const int r = idx / hp, c = idx % hp;
+        Xs[idx] = (r < nr && c < H) ? X[static_cast<size_t>(r) * H + c] : 0.f;
+      }
+    }
+    if (l > 0) stage_w(Ws, hp, p.w[l], H, H);
+    __syncthreads();
+    wgrad(Xs, xp, nin, Gc, hp, nr, H, out + of.w[l]);
+    if (rg == 0 && o < H) {
+      float sb = 0.f;
+      for (int r = 0; r < nr; ++r) sb += Gc[r * hp + o];
+      out[of.b[l] + o] = sb;
+    }
+    if (l > 0) {
+      const int i = o;
+      if (i < H) {
+        for (int r0b = rg * 8; r0b < GP; r0b += 32) {
+          float acc[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+          for (int oo = 0; oo < H; ++oo) {
+            const float wv = Ws[i * hp + oo];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = fmaf(Gc[(r0b + q) * hp + oo], wv, acc[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int r = r0b + q;
+            Gn[r * hp + i] = r < nr ? acc[q] * elu_d_out(Xs[r * hp + i]) : 0.f;
+          }
+        }
+      }
+      float* t = Gc;
+      Gc = Gn;
+      Gn = t;
+    }
+  }
+}
+
+// red [n] (the reduced slab row) -> the caller's gradient tensors; the conv kernel's sample channel gets 0
+__global__ void feat_scatter_kernel(const float* __restrict__ red, int Cin, int H, int k, float* gw0, float* gb0,
+                                    float* gw1, float* gb1, float* gw2, float* gb2, float* gw3, float* gb3,
+                                    float* gcw, float* gcb) {
+  const Off of = offsets(Cin, H, k);
+  float* gw[4] = {gw0, gw1, gw2, gw3};
+  float* gb[4] = {gb0, gb1, gb2, gb3};
+  const int n_cw = k * (1 + H) * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < of.n - k * H * H + n_cw; i += gridDim.x * blockDim.x) {
+    if (i < of.cw) {
+      int l = 3;
+      while (l > 0 && i < of.w[l]) --l;
+      if (i < of.b[l]) gw[l][i - of.w[l]] = red[i];
+      else gb[l][i - of.b[l]] = red[i];
+    } else if (i < of.cw + n_cw) {
+      const int e = i - of.cw, j = e / ((1 + H) * H), c = (e / H) % (1 + H), oo = e % H;
+      gcw[e] = c == 0 ? 0.f : red[of.cw + (j * H + c - 1) * H + oo];
+    } else {
+      gcb[i - of.cw - n_cw] = red[of.cb + i - of.cw - n_cw];
+    }
+  }
+}
+
+static size_t fwd_smem(const Args& a) {
+  const int RP = rows_pad(a.s * (kT - 1) + a.k), hp = a.H + 1, wp = std::max(a.Cin, a.H) + 1;
+  return static_cast<size_t>(RP * wp + RP * hp + wp * hp) * sizeof(float);
+}
+static size_t bwd_smem(const Args& a) {
+  const int hp = a.H + 1, ip = a.Cin + 1;
+  const int nd = kT + (a.k - 1 + a.s - 1) / a.s + 1;   // upper bound of the staged dC rows
+  const int DP = rows_pad(nd), FP = rows_pad(a.s * (kT - 1) + a.k), GP = rows_pad(a.s * kT);
+  return static_cast<size_t>(DP * hp + FP * hp + 2 * GP * hp + GP * std::max(ip, hp) + std::max(a.Cin, a.H) * hp) *
+         sizeof(float);
+}
+
+// dynamic LDS above the default 64 KB (the backward at k = 20 / 50 takes 70-85 KB): raise the kernels' limit once
+static int allow_lds() {
+  static int rc = [] {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(feat_fwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(feat_bwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return 1;
+    return 0;
+  }();
+  return rc;
+}
+
+static int make(const VissmFeatDesc* d, Args* a) {
+  VISSM_CHECK_ARG(d && d->n_win >= 1 && d->Lf >= 1 && d->Cin >= 1 && d->Cin <= kMaxCin && d->H >= 1 &&
+                      d->H <= kMaxH && d->k >= 1 && d->k <= kMaxK && (d->stride == 1 || d->stride == 2),
+                  "feat: bad shape (n_win >= 1, Cin <= %d, H <= %d, k <= %d, stride 1 | 2)", kMaxCin, kMaxH, kMaxK);
+  a->n_win = d->n_win;
+  a->Lf = d->Lf;
+  a->Cin = d->Cin;
+  a->H = d->H;
+  a->k = d->k;
+  a->s = d->stride;
+  a->Lh = d->Lh;
+  VISSM_CHECK_ARG(d->Lh >= 1 && d->stride * (d->Lh - 1) + d->k <= d->Lf, "feat: Lh = %d needs s (Lh - 1) + k <= Lf = %d",
+                  d->Lh, d->Lf);
+  a->Lu = d->stride * (d->Lh - 1) + d->k;
+  a->in_ws = d->in_win_stride;
+  VISSM_CHECK_ARG(a->in_ws >= static_cast<int64_t>(d->Lf) * d->Cin || d->n_win == 1,
+                  "feat: windows of h0 overlap (in_win_stride < Lf Cin)");
+  return VISSM_OK;
+}
+
+static Params params(const VissmFeatParams* w) {
+  Params p;
+  for (int l = 0; l < 4; ++l) {
+    p.w[l] = w->w[l];
+    p.b[l] = w->b[l];
+  }
+  p.cw = w->conv_w;
+  p.cb = w->conv_b;
+  return p;
+}
+
+}  // namespace feat
+}  // namespace vissm
+
+using namespace vissm;
+
+extern "C" {
+
+size_t vissm_feat_workspace_size(const VissmFeatDesc* d) {
+  feat::Args a;
+  if (feat::make(d, &a)) return 0;
+  const int nb = (a.Lu + a.s * feat::kT - 1) / (a.s * feat::kT);
+  const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
+  return align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)) + align_up(of.n * sizeof(float));
+}
+
+int vissm_feat_fwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float* h0, float* C, float* act,
+                   void* stream) {
+  feat::Args a;
+  int rc = feat::make(d, &a);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && h0 && C && act, "feat_fwd: null pointer");
+  if (feat::allow_lds()) {
+    set_error("feat_fwd: hipFuncSetAttribute failed");
+    return VISSM_ELAUNCH;
+  }
+  dim3 grid((a.Lh + feat::kT - 1) / feat::kT, a.n_win);
+  hipLaunchKernelGGL(feat::feat_fwd_kernel, grid, dim3(feat::kNT), feat::fwd_smem(a), as_stream(stream), a,
+                     feat::params(w), h0, C, act);
+  VISSM_CHECK_LAUNCH("feat_fwd");
+  return VISSM_OK;
+}
+
+int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float* h0, const float* act,
+                   const float* dC, const VissmFeatGrads* g, void* workspace, size_t ws_bytes, void* stream) {
+  feat::Args a;
+  int rc = feat::make(d, &a);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && h0 && act && dC && g, "feat_bwd: null pointer");
+  VISSM_CHECK_ARG(workspace && ws_bytes >= vissm_feat_workspace_size(d), "feat_bwd: workspace too small");
+  if (feat::allow_lds()) {
+    set_error("feat_bwd: hipFuncSetAttribute failed");
+    return VISSM_ELAUNCH;
+  }
+  hipStream_t st = as_stream(stream);
+  const int nb = (a.Lu + a.s * feat::kT - 1) / (a.s * feat::kT);
+  const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
+  float* slab = static_cast<float*>(workspace);
+  float* red = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                        align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)));
+  hipLaunchKernelGGL(feat::feat_bwd_kernel, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a), st, a,
+                     feat::params(w), h0, act, dC, slab);
+  VISSM_CHECK_LAUNCH("feat_bwd");
+  rc = launch_reduce_rows(slab, red, static_cast<int64_t>(a.n_win) * nb, of.n, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(feat::feat_scatter_kernel, dim3((of.n + a.k * a.H + 255) / 256), dim3(256), 0, st, red, a.Cin,
+                     a.H, a.k, g->w[0], g->b[0], g->w[1], g->b[1], g->w[2], g->b[2], g->w[3], g->b[3], g->conv_w,
+                     g->conv_b);
+  VISSM_CHECK_LAUNCH("feat_scatter");
+  return VISSM_OK;
+}
+
+}  // extern "C"

@@ -24,8 +24,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import (FlowShape, ma_flow, normal_base, normal_base_dev, base_logprob, elbo_terms, ElboFeeds,
-                  AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
+from .ops import (FlowShape, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
+                  ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, linear_bf16, linear_x3, tn_split_k
@@ -213,6 +213,22 @@ class IAF:
         lin = {"x3": linear_x3, "bf16": linear_bf16}.get(gemm, linear)
         G = lin(F, Wcat).view(nw, Lf, k, H)  # F may be a transposed view (LV)
         return (_DiagSum.apply(G.contiguous(), Lh, s) + self._p("conv/bias")).contiguous()
+
+    def window_conv(self, ts: torch.Tensor, Lh: int, s: int, gemm: Optional[str] = None) -> torch.Tensor:
+        """C = conv_shared(features(ts)): the first conv's window-shared part.  On the GPU, at kernel_len <= 16
+        (the AR configurations), the feature branch (a few thousand rows of [14] -> 50 -> 50 -> 50 -> 50, then the
+        k-tap conv) runs as one HIP launch each way (ops.feat_conv, vissm_feat_fwd / _bwd) instead of ~40 torch
+        launches per flow: AR-cfg step -0.25 ms.  The FHN (k = 20, stride 2) and SV (k = 50) shapes keep the library
+        GEMMs: their conv is a K = k H = 1000 / 2500 contraction the fp32 VALU kernel runs slower (FHN step +1.0 ms,
+        SV +6.1 ms, profiles/r04/ab_feat.log), and so do LV's time-mixing features ([kernel_ext - 1] channels).
+        VISSM_FEAT_TORCH=1 selects the torch form everywhere (A/B timing)."""
+        f = self.spec.feat
+        if ts.is_cuda and f == "mlp4" and self.spec.k <= 16 and os.environ.get("VISSM_FEAT_TORCH") != "1":
+            p = self._p
+            return feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
+                             p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
+                             p("conv/kernel"), p("conv/bias"))
+        return self.conv_shared(self.features(ts), Lh, s, gemm=gemm)
 
     def theta_factors(self, theta: torch.Tensor):
         """(theta, w_theta, b_theta) with theta_term = theta w_theta + b_theta: the collapsed weights _ThetaBranch
@@ -431,9 +447,8 @@ class Engine:
         L = md.kernel_ext
         for i, fl in enumerate(self.flows):
             ts = batch.ts if md.family == "lv" else batch.ts[:, i * md.k:, :]
-            F = fl.features(ts)
             Lh = (L - md.k) // s
-            C = fl.conv_shared(F, Lh, s, gemm=self.feature_gemm())
+            C = fl.window_conv(ts, Lh, s, gemm=self.feature_gemm())
             tt = fl.theta_term(theta)
             pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
@@ -523,9 +538,8 @@ class Engine:
         B = eps.shape[0]
         L = md.kernel_ext
         for i, fl in enumerate(self.flows[:-1]):
-            F = fl.features(batch.ts[:, i * md.k:, :])
             Lh = L - md.k
-            C = fl.conv_shared(F, Lh, 1)
+            C = fl.window_conv(batch.ts[:, i * md.k:, :], Lh, 1)
             tt = fl.theta_term(theta)
             pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
@@ -536,8 +550,7 @@ class Engine:
             L -= md.k
         fl = self.flows[-1]
         i = md.n_flows - 1
-        F = fl.features(batch.ts[:, i * md.k:, :])
-        C = fl.conv_shared(F, L - md.k, 1)
+        C = fl.window_conv(batch.ts[:, i * md.k:, :], L - md.k, 1)
         tt = fl.theta_term(theta)
         shape = self._last_shape(batch, B)
         w_eps, w_hid, b_hid, _, _, w_head, b_head = fl.weights()

@@ -167,6 +167,62 @@ def _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf=None) -> Fl
                       ptr(th), ptr(wt), ptr(bt), int(th.shape[1]))
 
 
+# ---------------------------------------------------------------------------------------
+# window-shared feature branch + the first conv's feature channels (vissm_feat_fwd / _bwd)
+# ---------------------------------------------------------------------------------------
+class FeatConvFn(torch.autograd.Function):
+    """C [n_win, Lh, H] = conv_b + the feature channels of the first conv over F = the four dense + ELU layers
+    of the window's time features h0 [n_win, Lf, Cin] (AR.py:53-62; SV_dense.py:53-62; fitz_nag_NVP.py:71-79), one
+    HIP launch each way (the torch form is ~40 small launches per flow).  The gradient reaches the four dense
+    layers and the conv kernel (its sample channel 0 gets zero here: that part is the flow kernel's w_eps) and
+    bias; h0 is data."""
+
+    @staticmethod
+    def forward(ctx, h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+        ws = (W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+        _require_gpu(*ws)
+        n_win, Lf, Cin = h0.shape
+        if not h0.is_cuda or h0.dtype != torch.float32 or h0.stride(2) != 1 or h0.stride(1) != Cin:
+            h0 = h0.contiguous()
+            _require_gpu(h0)
+        H, k = W3.shape[1], conv_w.shape[0]
+        d = _lib.FeatDesc(n_win, Lf, Cin, H, k, s, Lh, h0.stride(0) if n_win > 1 else Lf * Cin)
+        p = _feat_params(ws)
+        C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=h0.device)
+        act = torch.empty(4, n_win, Lf, H, dtype=torch.float32, device=h0.device)
+        check(_lib.load().vissm_feat_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(C), ptr(act),
+                                         _lib.stream_handle(h0.device)), "vissm_feat_fwd")
+        ctx.save_for_backward(h0, act, *ws)
+        ctx.desc = d
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        h0, act, *ws = ctx.saved_tensors
+        d = ctx.desc
+        dC = dC.contiguous()
+        gr = [torch.empty_like(t) for t in ws]
+        g = _lib.FeatGrads((ctypes.c_void_p * 4)(*[ptr(t) for t in gr[0:8:2]]),
+                           (ctypes.c_void_p * 4)(*[ptr(t) for t in gr[1:8:2]]), ptr(gr[8]), ptr(gr[9]))
+        lib = _lib.load()
+        nb = lib.vissm_feat_workspace_size(ctypes.byref(d))
+        if nb == 0:
+            raise _lib.VissmError(f"vissm_feat_workspace_size failed: {lib.vissm_last_error().decode()}")
+        wsb = _workspace(nb, dC.device)
+        check(lib.vissm_feat_bwd(ctypes.byref(d), ctypes.byref(_feat_params(ws)), ptr(h0), ptr(act), ptr(dC),
+                                 ctypes.byref(g), ptr(wsb), nb, _lib.stream_handle(dC.device)), "vissm_feat_bwd")
+        return (None, None, None, *gr)
+
+
+def _feat_params(ws) -> "_lib.FeatParams":
+    return _lib.FeatParams((ctypes.c_void_p * 4)(*[ptr(t) for t in ws[0:8:2]]),
+                           (ctypes.c_void_p * 4)(*[ptr(t) for t in ws[1:8:2]]), ptr(ws[8]), ptr(ws[9]))
+
+
+def feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+    return FeatConvFn.apply(h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+
+
 class MAFlowFn(torch.autograd.Function):
     """One IAF flow (IAF._create_flow, AR.py:50-85) -> (u_next, logsig)."""
 
