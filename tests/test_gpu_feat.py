@@ -51,6 +51,7 @@ def _case(n_win, Lf, Cin, H, k, s, seed, sv=False):
 
 
 def _rel(a, b):
+    a, b = a.detach(), b.detach()
     return float((a - b).double().norm() / b.double().norm().clamp_min(1e-30))
 
 
