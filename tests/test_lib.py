@@ -225,3 +225,15 @@ def test_feat_workspace_size_validates_without_gpu():
     for bad in [(1, 5024, 14, 65, 8, 1, 5017, 0), (1, 5024, 64, 50, 8, 1, 5017, 0), (1, 5024, 14, 50, 65, 1, 4960, 0),
                 (1, 5024, 14, 50, 8, 3, 1000, 0), (1, 5024, 14, 50, 8, 1, 5018, 0), (2, 100, 14, 50, 8, 1, 93, 99 * 14)]:
         assert lib.vissm_feat_workspace_size(ctypes.byref(_lib.FeatDesc(*bad))) == 0, bad
+
+
+def test_asm_mfma_accumulators_hazard_free():
+    """The three-layer backward's weight-gradient accumulators live in AGPRs through inline-asm MFMAs (hipcc pads no
+    hazard for an asm statement): in the device assembly of flow_v5n.hip no compiler instruction touches an AGPR that
+    an asm MFMA wrote fewer than 12 wait states earlier on any path (scripts/check_agpr_asm.py; ~1 min of hipcc)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_agpr_asm.py")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "bwd2n_kernel" in r.stdout

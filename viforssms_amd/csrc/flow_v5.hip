@@ -86,6 +86,45 @@ __device__ __forceinline__ f4 mfma16(bf4 a, bf4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a), __builtin_bit_cast(s4, b), c, 0, 0, 0);
 }
 
+// the three-layer backward's accumulators in AGPRs (below): on in flow_v5n.hip, the translation unit built with the
+// VGPR-form MFMAs that runs those kernels
+#ifndef VISSM_BWD2N_AACC
+#define VISSM_BWD2N_AACC 0
+#endif
+// accumulator-file MFMAs (inline asm): C / D pinned to AGPRs ("+a"), A / B in VGPRs.  For item-lifetime weight-gradient
+// accumulators that only MFMAs touch, beside a chain that needs the 256 VGPRs (bwd2n_kernel).  hipcc pads no hazard
+// inside the string: the opening s_nop 1 covers a VALU / v_accvgpr_write producer of an operand; accumulating into the
+// previous MFMA's D needs none; readers of D after the loop wait through agpr_drain4().
+__device__ __forceinline__ void mfma32_a(bf8 a, bf8 b, f4& c) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_a4(bf8 a, const bf8 (&b)[4], f4& c0, f4& c1, f4& c2, f4& c3) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %4, %5, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %4, %6, %1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %2, %4, %7, %2\n\t"
+      "v_mfma_f32_16x16x32_bf16 %3, %4, %8, %3"
+      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+      : "v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+}
+// the same with a shared B operand: c_x = A_x B
+__device__ __forceinline__ void mfma32_a4b(const bf8 (&a)[4], bf8 b, f4& c0, f4& c1, f4& c2, f4& c3) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %4, %8, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %1, %5, %8, %1\n\t"
+      "v_mfma_f32_16x16x32_bf16 %2, %6, %8, %2\n\t"
+      "v_mfma_f32_16x16x32_bf16 %3, %7, %8, %3"
+      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b));
+}
+// 12 wait states (an 8-pass MFMA's D before any non-MFMA reader), tied to the accumulators so that no read of them can
+// be scheduled above it
+__device__ __forceinline__ void agpr_drain4(f4& c0, f4& c1, f4& c2, f4& c3) {
+  asm volatile("s_nop 7\n\ts_nop 3" : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3));
+}
+
 template <int NP>
 __device__ __forceinline__ f4 mm(const Fr8<NP>& a, const Fr8<NP>& b, f4 c) {
   if constexpr (NP >= 2) c = mfma32(a.l, b.h, c);  // a: the weight operand
@@ -2113,6 +2152,10 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
   // dcon rows: k <= 24 (JB <= 2) at column s p + j of row j (padded: du[q] = sum_j row_j[q], no masks); k > 32 in
   // [j][p] rows of stride P + 1 (no room for padded rows), summed along the diagonal q = p + j (at most P terms)
   constexpr bool DIAG = JB > 2;
+  // dW / dW_eps / dW_head accumulate in AGPRs through inline asm (mfma32_a*) at k <= 32; at k > 32 (SV) the compiler
+  // copies those operands between register files around the statements (scripts/check_agpr_asm.py finds the copies
+  // within an MFMA's wait states), so the builtin form stays there
+  constexpr bool AACC = VISSM_BWD2N_AACC && JB <= 2;
   constexpr int KR = JB == 1 ? 16 : JB == 2 ? 24 : KP;
   constexpr int QWR = DIAG ? P + 1 : s * P + KR;
   constexpr int UWN = KB == 1 ? 64 : 128;    // u entries staged per sample (s P + k of them read)
@@ -2298,8 +2341,12 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         bf8 i1f[4];
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) i1f[hb] = tr_frag2(im0, hb, g, c);
+        if constexpr (AACC) {
+          mfma32_a4b(i1f, i1f[3], dWh[0], dWh[1], dWh[2], dWh[3]);
+        } else {
 #pragma unroll
-        for (int hb = 0; hb < 4; ++hb) dWh[hb] = mfma32(i1f[hb], i1f[3], dWh[hb]);
+          for (int hb = 0; hb < 4; ++hb) dWh[hb] = mfma32(i1f[hb], i1f[3], dWh[hb]);
+        }
       }
       f4 D[2][4];
       {
@@ -2355,8 +2402,12 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int ib = 0; ib < 4; ++ib) {
             const bf8 xa = tr_frag2(im0, ib, g, c);
+            if constexpr (AACC) {
+              mfma32_a4(xa, dzf, dW[l][ib][0], dW[l][ib][1], dW[l][ib][2], dW[l][ib][3]);
+            } else {
 #pragma unroll
-            for (int ob = 0; ob < 4; ++ob) dW[l][ib][ob] = mfma32(xa, dzf[ob], dW[l][ib][ob]);
+              for (int ob = 0; ob < 4; ++ob) dW[l][ib][ob] = mfma32(xa, dzf[ob], dW[l][ib][ob]);
+            }
           }
         }
 #pragma unroll
@@ -2413,7 +2464,10 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
           const bf8 ta = tr_frag2(im1, hb, g, c);
           dth4[hb] = mfma32(ta, ones_ab, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-          for (int jb = 0; jb < JB; ++jb) dWe[jb][hb] = mfma32(uaf[jb], ta, dWe[jb][hb]);
+          for (int jb = 0; jb < JB; ++jb) {
+            if constexpr (AACC) mfma32_a(uaf[jb], ta, dWe[jb][hb]);
+            else dWe[jb][hb] = mfma32(uaf[jb], ta, dWe[jb][hb]);
+          }
         }
       }
       if (c == 0 || (c == 8 && two)) {
@@ -2518,6 +2572,16 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
       }
     }
     if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
+  }
+  if constexpr (AACC) {
+    // the accumulators leave the AGPRs only through these statements: their wait states precede every read
+#pragma unroll
+    for (int l = 0; l < NH; ++l)
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib) agpr_drain4(dW[l][ib][0], dW[l][ib][1], dW[l][ib][2], dW[l][ib][3]);
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb) agpr_drain4(dWe[jb][0], dWe[jb][1], dWe[jb][2], dWe[jb][3]);
+    agpr_drain4(dWh[0], dWh[1], dWh[2], dWh[3]);
   }
   const int H = a.H;
   const int nW = a.k * H + NH * H * H + 3 * NH * H + 2 * H + 2;
