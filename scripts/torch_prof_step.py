@@ -1,6 +1,6 @@
 """Op-level breakdown of the benchmarked training step (torch.profiler on the GPU): which torch ops
 around the HIP kernels cost device time, grouped by op and input shape.
-usage: python scripts/torch_prof_step.py [--precision bf16] [--rows 40]"""
+usage: python scripts/torch_prof_step.py [--model ar|lv|sv|fhn] [--precision bf16] [--rows 40]"""
 import argparse
 import os
 import sys
@@ -14,9 +14,10 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--model", default="ar")
     ap.add_argument("--rows", type=int, default=45)
     a = ap.parse_args()
-    args = bench.parse_args(["--precision", a.precision])
+    args = bench.parse_args(["--precision", a.precision, "--model", a.model])
     from viforssms_amd import _lib
     from viforssms_amd.launch import init_distributed
     ctx = init_distributed()

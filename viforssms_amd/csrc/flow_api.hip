@@ -39,6 +39,15 @@ int flow5_bwd_nh3(const VissmFlowDesc*, const VissmFlowParams*, const float*, co
                   const float*, const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*,
                   size_t, hipStream_t);
 
+// and for k > 32 at three hidden layers (flow_v5s.hip)
+void flow5_geometry_nh3s(const VissmFlowDesc* d, int which, int32_t* out);
+size_t flow5_workspace_size_nh3s(const VissmFlowDesc* d, int backward);
+int flow5_fwd_nh3s(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*,
+                   const float*, float*, float*, void*, size_t, hipStream_t);
+int flow5_bwd_nh3s(const VissmFlowDesc*, const VissmFlowParams*, const float*, const float*, const int32_t*,
+                   const float*, const float*, const float*, float*, float*, float*, const VissmFlowGrads*, void*,
+                   size_t, hipStream_t);
+
 bool flow5_ar_fused_supports(const VissmFlowDesc* d);
 size_t flow5_ar_fused_workspace_size(const VissmFlowDesc* d);
 int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -71,10 +80,12 @@ static int validate(const VissmFlowDesc* d) {
 // than requested).
 static bool use_v5(const VissmFlowDesc* d) { return d->precision != VISSM_PREC_FP32 && flow5_supports(d); }
 // three hidden layers on one window with the two-sample backward's k (LV, FHN: k <= 24; SV: 32 < k <= 64, stride 1): the
-// build without the SLP vectorizer (flow_v5n.hip; LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5, SV 7.2 -> 6.7 ms
-// per launch).  The one-sample three-layer kernel (several windows) measured slower that way (SV: 10.3 -> 10.8 ms).
-static bool use_nh3(const VissmFlowDesc* d) {
-  return d->n_hidden == 3 && d->n_win == 1 && (d->k <= 24 || (d->k > 32 && d->k <= 64 && !d->stride2));
+// builds without the SLP vectorizer (LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5, SV 7.2 -> 6.7 ms per launch),
+// k <= 24 in flow_v5n.hip (also VGPR-form MFMAs and AGPR accumulators: LV 16.6 -> 14.6 ms), k > 32 in flow_v5s.hip.
+// The one-sample three-layer kernel (several windows) measured slower without the vectorizer (SV: 10.3 -> 10.8 ms).
+static bool use_nh3(const VissmFlowDesc* d) { return d->n_hidden == 3 && d->n_win == 1 && d->k <= 24; }
+static bool use_nh3s(const VissmFlowDesc* d) {
+  return d->n_hidden == 3 && d->n_win == 1 && d->k > 32 && d->k <= 64 && !d->stride2;
 }
 
 }  // namespace vissm
@@ -85,7 +96,9 @@ extern "C" {
 
 size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward) {
   if (validate(d) != VISSM_OK) return 0;
-  if (use_v5(d)) return use_nh3(d) ? flow5_workspace_size_nh3(d, backward) : flow5_workspace_size(d, backward);
+  if (use_v5(d))
+    return use_nh3(d) ? flow5_workspace_size_nh3(d, backward)
+         : use_nh3s(d) ? flow5_workspace_size_nh3s(d, backward) : flow5_workspace_size(d, backward);
   return use_flow4(d) ? flow4_workspace_size(d, backward) : flow2_workspace_size(d, backward);
 }
 
@@ -97,7 +110,7 @@ int vissm_flow_geometry(const VissmFlowDesc* d, int32_t which, int32_t* out) {
     VISSM_CHECK_ARG(flow5_ar_fused_supports(d), "flow_geometry: the descriptor has no fused AR(1) last flow");
     flow5_geometry(d, 2, out);
   } else if (use_v5(d)) {
-    (use_nh3(d) ? flow5_geometry_nh3 : flow5_geometry)(d, which, out);
+    (use_nh3(d) ? flow5_geometry_nh3 : use_nh3s(d) ? flow5_geometry_nh3s : flow5_geometry)(d, which, out);
   } else {
     (use_flow4(d) ? flow4_geometry : flow2_geometry)(d, which, out);
   }
@@ -118,8 +131,8 @@ int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                   "flow_fwd: VISSM_PREC_BF16X2_BF16 is a precision of vissm_flow_ar_elbo_fused only");
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
-    return (use_nh3(d) ? flow5_fwd_nh3 : flow5_fwd)(d, w, u, C, win, theta_term, u_next, logsig, workspace,
-                                                          ws_bytes, st);
+    return (use_nh3(d) ? flow5_fwd_nh3 : use_nh3s(d) ? flow5_fwd_nh3s : flow5_fwd)(d, w, u, C, win, theta_term, u_next,
+                                                                                    logsig, workspace, ws_bytes, st);
   if (use_flow4(d)) return flow4_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
   return flow2_fwd(d, w, u, C, win, theta_term, u_next, logsig, workspace, ws_bytes, st);
 }
@@ -142,8 +155,9 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_bwd: n_win > 1 needs win[]");
   hipStream_t st = as_stream(stream);
   if (use_v5(d))
-    return (use_nh3(d) ? flow5_bwd_nh3 : flow5_bwd)(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC,
-                                                          dtheta_term, gr, workspace, ws_bytes, st);
+    return (use_nh3(d) ? flow5_bwd_nh3 : use_nh3s(d) ? flow5_bwd_nh3s : flow5_bwd)(d, w, u, C, win, theta_term,
+                                                                                    du_next, dlogsig, du, dC, dtheta_term,
+                                                                                    gr, workspace, ws_bytes, st);
   if (use_flow4(d))
     return flow4_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
   return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
