@@ -237,3 +237,26 @@ def test_asm_mfma_accumulators_hazard_free():
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "bwd2n_kernel" in r.stdout
+
+
+def test_agpr_audit_detects_unpadded_reads(tmp_path):
+    """scripts/check_agpr_asm.py is not vacuous: on a synthetic kernel it flags a compiler read of an AGPR an asm MFMA
+    just wrote, across a fall-through and a branch edge, and passes once a drain statement sits in between."""
+    import subprocess
+    import sys
+
+    def kernel(between):
+        return "\n".join(["_Z4testv:", "; %bb.0:", ";;#ASMSTART", "s_nop 1",
+                          "v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[4:7], a[0:3]", ";;#ASMEND", *between,
+                          "s_cbranch_scc1 .LBB0_2", "; %bb.1:", "v_add_f32_e32 v9, v9, v9", ".LBB0_2:",
+                          "v_accvgpr_read_b32 v8, a1", "s_endpgm", ".Lfunc_end0:", ""])
+    bad = tmp_path / "bad.s"
+    bad.write_text(kernel([]))
+    good = tmp_path / "good.s"
+    good.write_text(kernel([";;#ASMSTART", "s_nop 7", "s_nop 3", ";;#ASMEND"]))
+    far = tmp_path / "far.s"
+    far.write_text(kernel(["v_add_f32_e32 v9, v9, v9"] * 12))
+    script = os.path.join(ROOT, "scripts", "check_agpr_asm.py")
+    assert subprocess.run([sys.executable, script, str(bad)], capture_output=True).returncode == 1
+    assert subprocess.run([sys.executable, script, str(good)], capture_output=True).returncode == 0
+    assert subprocess.run([sys.executable, script, str(far)], capture_output=True).returncode == 0
