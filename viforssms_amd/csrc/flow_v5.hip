@@ -1941,8 +1941,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // forward): hi planes register-resident, lo planes read from LDS per use
 // NH / JB: one hidden layer (AR) or three with the BN affine folded (LV / SV / FHN heads: stride-2 head with the
 // pass-through of the even outputs and the fused pair swap), k <= 32 (one layer-0 K block)
-template <bool TF, int NP, int NH, int JB>
-__global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __restrict__ u,
+template <bool TF, int NP, int NH, int JB, int NWF = NW>
+__global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
                                                                   const bf8* __restrict__ img,
@@ -1952,8 +1952,8 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
                                                                   const u4* __restrict__ thf) {
   constexpr int KB = (JB + 1) / 2;  // layer-0 K blocks (k > 32: two, a 128-entry u window)
   __shared__ Shared<NH, KB, JB, NP> sh;
-  __shared__ float uwin[NW][2][64 * KB];
-  load_shared(sh, img, cst);
+  __shared__ float uwin[NWF][2][64 * KB];
+  load_shared<NH, KB, JB, NP, 64 * NWF>(sh, img, cst);
   {  // static wave priority = dispatch round mod 4 (as fwd_kernel)
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.x / a.ncu) & 3;
     if (r == 1) __builtin_amdgcn_s_setprio(1);
@@ -1962,23 +1962,29 @@ __global__ __launch_bounds__(NT, 2) void fwd2_kernel(KArgs a, const float* __res
   }
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + w);
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * NWF + w);
   if (item >= a.n_items) return;
   const int grp = item / a.n_chunks, ch = item % a.n_chunks;
   const int m_lo = ch * a.CH, m_hi = min(a.Lh, m_lo + a.CH);
   const int b_lo = grp * a.S, nb = min(a.S, a.B - b_lo);
-  constexpr int NWR = 8 * NH + 4 * KB + 2;
+  // weight hi planes register-resident in 4-wave blocks; 8-wave blocks read every plane from LDS (fewer registers, and
+  // the block's LDS image serves twice the waves)
+  constexpr bool HIREG = NWF == NW;
+  constexpr int NWR = HIREG ? 8 * NH + 4 * KB + 2 : 1;
   bf8 wr[NWR];
+  if constexpr (HIREG) {
 #pragma unroll
-  for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
+    for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
 #pragma unroll
-  for (int i = 0; i < 4 * KB; ++i) wr[8 * NH + i] = sh.img[16 * NH + i][0][lane];
+    for (int i = 0; i < 4 * KB; ++i) wr[8 * NH + i] = sh.img[16 * NH + i][0][lane];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
+    for (int i = 0; i < 2; ++i) wr[8 * NH + 4 * KB + i] = sh.img[16 * NH + 4 * KB + 2 * JB + i][0][lane];
+  }
   // fragment f: its hi plane's register copy (index i); NP = 2: with its lo plane from LDS
   auto W = [&](int f, int i) -> Fr8<NP> {
     Fr8<NP> r;
-    r.h = wr[i];
+    if constexpr (HIREG) r.h = wr[i];
+    else r.h = sh.img[f][0][lane];
     if constexpr (NP == 2) r.l = sh.img[f][1][lane];
     return r;
   };
@@ -2920,9 +2926,17 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   dim3 grid((g.n_items + NW - 1) / NW);
   prof_begin(VISSM_PROF_FLOW_FWD, st);
   if (f2) {
-#define FWD2_LAUNCH(TF_, NP_, NH_, JB_)                                                                           \
-  hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_>), grid, dim3(NT), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, \
-                     u_next, ws.ls_slab, ws.thf)
+// 8-wave blocks with every weight plane read from LDS for the split-weight forward (155 -> 93 VGPRs: bf16x2 forward
+// 9.81 -> 9.19 ms per AR-cfg launch) and three hidden layers (225 -> 126: LV 3.68 -> 3.51 ms, FHN 0.77 -> 0.69 ms): the
+// block's weight image then serves twice the waves and the LDS no longer caps them at 2-3 per SIMD; the bf16 AR forward
+// keeps 4-wave blocks with register-resident hi planes (8-wave blocks: 6.90 -> 7.16 ms, still four waves per SIMD at
+// 103 VGPRs), profiles/r04/ab_fwd_blocks_steps.log
+#define FWD2_LAUNCH(TF_, NP_, NH_, JB_)                                                                            \
+  do {                                                                                                           \
+    constexpr int nwf = (NP_ == 2 || NH_ == 3) ? 8 : NW;                                                           \
+    hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_, nwf>), dim3((g.n_items + nwf - 1) / nwf), dim3(64 * nwf), \
+                       0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, ws.ls_slab, ws.thf);                   \
+  } while (0)
     const int jb = jb_of(d->k);
     if (d->n_hidden == 3) {
       if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1);
