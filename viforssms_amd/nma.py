@@ -221,9 +221,10 @@ class IAF:
         launches per flow: AR-cfg step -0.25 ms.  The FHN (k = 20, stride 2) and SV (k = 50) shapes keep the library
         GEMMs: their conv is a K = k H = 1000 / 2500 contraction the fp32 VALU kernel runs slower (FHN step +1.0 ms,
         SV +6.1 ms, profiles/r04/ab_feat.log), and so do LV's time-mixing features ([kernel_ext - 1] channels).
-        VISSM_FEAT_TORCH=1 selects the torch form everywhere (A/B timing)."""
+        VISSM_FEAT_TORCH=1 selects the torch form everywhere, VISSM_FEAT_MAX_K moves the kernel_len bound (A/B timing)."""
         f = self.spec.feat
-        if ts.is_cuda and f == "mlp4" and self.spec.k <= 16 and os.environ.get("VISSM_FEAT_TORCH") != "1":
+        kmax = int(os.environ.get("VISSM_FEAT_MAX_K", "16"))
+        if ts.is_cuda and f == "mlp4" and self.spec.k <= kmax and os.environ.get("VISSM_FEAT_TORCH") != "1":
             p = self._p
             return feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
                              p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
