@@ -104,6 +104,11 @@ typedef struct {
                           a work item (the kernel's tile size; raised to the halo minimum).  Lets a
                           small batch run the chunk geometry of a large one: a parity test at B = 20
                           walks the ~160-tile chunks the B = 65536 benchmark launch walks. */
+  int32_t u_pitch;    /* row stride of u and du in floats (0 = L; else >= L).  A caller that pads rows to
+                         16 floats (64 bytes) gets aligned du stores from the t-chunks of the two-sample
+                         bf16 backward, which otherwise straddle 32-byte write sectors (+55 % du bytes). */
+  int32_t out_pitch;  /* row stride of u_next / du_next in floats (0 = L - k; else >= L - k); the fused
+                         AR(1) last flow writes x dense [B][M+1] and takes 0 or L - k */
 } VissmFlowDesc;
 
 typedef struct {

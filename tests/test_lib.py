@@ -207,7 +207,7 @@ def test_abi_struct_layouts_match_ctypes():
     f = lib.vissm_host_abi_layout
     f.restype = None
     f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
-    for which, (cls, last) in enumerate([(_lib.FlowDesc, "chunk_tiles"), (_lib.FlowParams, "theta_rank"),
+    for which, (cls, last) in enumerate([(_lib.FlowDesc, "out_pitch"), (_lib.FlowParams, "theta_rank"),
                                          (_lib.FlowGrads, "b_head")]):
         out = (ctypes.c_size_t * 2)()
         f(which, out)

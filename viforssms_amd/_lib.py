@@ -41,7 +41,8 @@ _size_t = ctypes.c_size_t
 
 class FlowDesc(ctypes.Structure):
     _fields_ = [(n, _i32) for n in ("B", "L", "k", "H", "n_hidden", "bn", "stride2", "swap_out",
-                                    "n_logsig", "n_win", "precision", "chunk_tiles")]
+                                    "n_logsig", "n_win", "precision", "chunk_tiles", "u_pitch",
+                                    "out_pitch")]
 
 
 class FlowParams(ctypes.Structure):

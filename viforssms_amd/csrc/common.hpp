@@ -114,7 +114,8 @@ int launch_reduce_rows_inplace(float* slab, float* out, int64_t R, int64_t N, hi
 int launch_reduce_rows_bf16(const void* slab, float* out, int64_t R, int64_t N, hipStream_t st);
 
 // flow epilogues shared by the flow implementations (flow_common.hip)
-int launch_halo_fixup(float* du, const float* halo, int B, int L, int k, int n_chunks, int s, int CH, hipStream_t st);
+int launch_halo_fixup(float* du, const float* halo, int B, int L, int pL, int k, int n_chunks, int s, int CH,
+                      hipStream_t st);
 int launch_reduce_by_window(const float* slab, const int32_t* win, float* out, int B, int n_win, int64_t N,
                             hipStream_t st);
 int launch_scatter_wgrad(const float* red, const VissmFlowGrads* g, int k, int H, int nh, int bn, hipStream_t st);

@@ -72,6 +72,9 @@ static int validate(const VissmFlowDesc* d) {
                       d->precision == VISSM_PREC_BF16X2_BF16,
                   "flow: unknown precision %d", d->precision);
   VISSM_CHECK_ARG(d->chunk_tiles >= 0, "flow: chunk_tiles=%d must be >= 0 (0 = automatic)", d->chunk_tiles);
+  VISSM_CHECK_ARG(d->u_pitch == 0 || d->u_pitch >= d->L, "flow: u_pitch=%d must be 0 or >= L=%d", d->u_pitch, d->L);
+  VISSM_CHECK_ARG(d->out_pitch == 0 || d->out_pitch >= d->L - d->k, "flow: out_pitch=%d must be 0 or >= L - k=%d",
+                  d->out_pitch, d->L - d->k);
   return VISSM_OK;
 }
 
@@ -188,6 +191,8 @@ int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, c
   VISSM_CHECK_ARG(gr->w_eps && gr->w_hid && gr->b_hid && gr->w_head && gr->b_head, "flow_ar_elbo_fused: null grad");
   VISSM_CHECK_ARG(d->n_win == 1 || win, "flow_ar_elbo_fused: n_win > 1 needs win[]");
   VISSM_CHECK_ARG(obs_std > 0.f, "flow_ar_elbo_fused: obs_std must be positive");
+  VISSM_CHECK_ARG(d->out_pitch == 0 || d->out_pitch == d->L - d->k, "flow_ar_elbo_fused: x is written dense (out_pitch "
+                  "%d must be 0 or L - k)", d->out_pitch);
   return flow5_ar_fused(d, w, u, C, win, theta_term, theta, obs, obs_bin, obs_std, scale, x, logsig, du, dC,
                         dtheta_term, gr, workspace, ws_bytes, as_stream(stream));
 }

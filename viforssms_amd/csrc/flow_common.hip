@@ -8,14 +8,14 @@ namespace vissm {
 
 namespace {
 
-// du[b][s*(c+1)*CH + q] += halo[b][c][q]: the transposed-conv overhang of t-chunk c into c + 1
-__global__ void halo_fixup_kernel(float* __restrict__ du, const float* __restrict__ halo, int B, int L, int k,
+// du[b][s*(c+1)*CH + q] += halo[b][c][q]: the transposed-conv overhang of t-chunk c into c + 1 (rows pL apart)
+__global__ void halo_fixup_kernel(float* __restrict__ du, const float* __restrict__ halo, int B, int L, int pL, int k,
                                   int n_chunks, int s, int CH) {
   const int b = blockIdx.x;
   for (int i = threadIdx.x; i < (n_chunks - 1) * k; i += blockDim.x) {
     const int c = i / k, q = i % k;
     const int pos = s * (c + 1) * CH + q;
-    if (pos < L) du[static_cast<size_t>(b) * L + pos] += halo[(static_cast<size_t>(b) * n_chunks + c) * k + q];
+    if (pos < L) du[static_cast<size_t>(b) * pL + pos] += halo[(static_cast<size_t>(b) * n_chunks + c) * k + q];
   }
 }
 
@@ -54,9 +54,10 @@ __global__ void scatter_wgrad_kernel(const float* __restrict__ red, VissmFlowGra
 
 }  // namespace
 
-int launch_halo_fixup(float* du, const float* halo, int B, int L, int k, int n_chunks, int s, int CH, hipStream_t st) {
+int launch_halo_fixup(float* du, const float* halo, int B, int L, int pL, int k, int n_chunks, int s, int CH,
+                      hipStream_t st) {
   if (n_chunks <= 1) return VISSM_OK;
-  hipLaunchKernelGGL(halo_fixup_kernel, dim3(B), dim3(256), 0, st, du, halo, B, L, k, n_chunks, s, CH);
+  hipLaunchKernelGGL(halo_fixup_kernel, dim3(B), dim3(256), 0, st, du, halo, B, L, pL, k, n_chunks, s, CH);
   VISSM_CHECK_LAUNCH("flow_halo");
   return VISSM_OK;
 }

@@ -157,6 +157,7 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, WIm
 
 struct KArgs {
   int B, L, k, H, bn, s, swap_out, n_logsig, n_win, Lout, Lh, CH, n_chunks, S;
+  int pL, pLo;  // row strides of u / du and u_next / du_next (VissmFlowDesc.u_pitch / out_pitch)
   int KS;  // k-steps of the sample-channel conv: ceil(k/4)
   int HK;  // k-steps over hidden units: ceil(H/4)
 };
@@ -330,8 +331,8 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
     const int b = g * a.S + bl;
     if (b >= a.B) break;
     const int wi = win ? win[b] : 0;
-    const float* ub = u + static_cast<size_t>(b) * a.L;
-    float* ob = u_next + static_cast<size_t>(b) * a.Lout;
+    const float* ub = u + static_cast<size_t>(b) * a.pL;
+    float* ob = u_next + static_cast<size_t>(b) * a.pLo;
     float ls_acc = 0.f;
     for (int m0 = m_lo; m0 < m_hi; m0 += P) {
       const int nP = min(P, m_hi - m0);
@@ -423,8 +424,8 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     for (int bl = 0; bl < nb; ++bl) {
       const int b = b_lo + bl;
       const int wi = win ? win[b] : 0;
-      const float* ub = u + static_cast<size_t>(b) * a.L;
-      const float* gb = gout + static_cast<size_t>(b) * a.Lout;
+      const float* ub = u + static_cast<size_t>(b) * a.pL;
+      const float* gb = gout + static_cast<size_t>(b) * a.pLo;
       __syncthreads();
       load_unit_inputs<NH>(a, sm, ub, tht + static_cast<size_t>(b) * a.H, t0);
       for (int q = tid; q < 2 * P; q += NT) {
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       __syncthreads();
       // du over local positions q in [0, s*nP + k)
       const int fin = a.s * nP;
-      float* db = du + static_cast<size_t>(b) * a.L;
+      float* db = du + static_cast<size_t>(b) * a.pL;
       for (int q = tid; q < fin + a.k; q += NT) {
         float v = 0.f;
         for (int j = 0; j < a.k; ++j) {
@@ -619,7 +620,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     for (int q = tid; q < a.k; q += NT) {
-      if (c == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = carry[bl][q];
+      if (c == a.n_chunks - 1) du[static_cast<size_t>(b) * a.pL + a.Lout + q] = carry[bl][q];
       else halo[(static_cast<size_t>(b) * a.n_chunks + c) * a.k + q] = carry[bl][q];
     }
     if (tid < a.H) dth_slab[(static_cast<size_t>(c) * a.B + b) * a.H + tid] = dth[bl][tid];
@@ -683,6 +684,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   KArgs a;
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.bn = d->bn; a.s = g.s; a.swap_out = d->swap_out;
+  a.pL = d->u_pitch ? d->u_pitch : d->L; a.pLo = d->out_pitch ? d->out_pitch : g.Lout;
   a.n_logsig = d->n_logsig; a.n_win = d->n_win; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks;
   a.S = g.S;
   a.KS = (d->k + 3) / 4;
@@ -777,7 +779,7 @@ int flow2_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   VISSM_CHECK_LAUNCH("flow2_bwd");
   prof_end(VISSM_PROF_FLOW_BWD_DU, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, a.pL, d->k, g.n_chunks, g.s, g.CH, st);
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {

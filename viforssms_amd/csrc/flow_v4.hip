@@ -170,6 +170,7 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, WIm
 
 struct KArgs {
   int B, L, k, H, bn, s, swap_out, n_logsig, n_win, Lout, Lh, CH, n_chunks, S;
+  int pL, pLo;  // row strides of u / du and u_next / du_next (VissmFlowDesc.u_pitch / out_pitch)
   int KS;  // k-steps of the sample-channel conv: ceil(k/4)
   int HK;  // k-steps over hidden units: ceil(H/4)
 };
@@ -275,11 +276,11 @@ __device__ __forceinline__ void prefetch(const KArgs& a, const float* __restrict
                                          const int32_t* __restrict__ win, int b, int t0, int nP, Pre& pf) {
   const int tid = threadIdx.x;
   const int span = a.s * P + a.k + 2;
-  pf.u = (tid < span && t0 + tid < a.L) ? u[static_cast<size_t>(b) * a.L + t0 + tid] : 0.f;
+  pf.u = (tid < span && t0 + tid < a.L) ? u[static_cast<size_t>(b) * a.pL + t0 + tid] : 0.f;
   pf.go = 0.f;
   if (gout && tid < a.s * nP) {
     const int o = t0 + tid;
-    pf.go = gout[static_cast<size_t>(b) * a.Lout + (a.swap_out ? (o ^ 1) : o)];
+    pf.go = gout[static_cast<size_t>(b) * a.pLo + (a.swap_out ? (o ^ 1) : o)];
   }
   pf.th = tid < a.H ? tht[static_cast<size_t>(b) * a.H + tid] : 0.f;
   pf.dls = (dls && tid == 0) ? dls[b] : 0.f;
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
         const int p = 16 * cb + L.li;
         if (p < nP) {
           const float sg = softplus_f(rr[cb]) + 1e-10f;
-          float* ob = u_next + static_cast<size_t>(b) * a.Lout;
+          float* ob = u_next + static_cast<size_t>(b) * a.pLo;
           const int o = t0 + a.s * p + (a.s - 1);
           ob[a.swap_out ? (o ^ 1) : o] = sm.us[a.s * p + (a.s - 1) + a.k] * sg + mu[cb];
           if (a.s == 2) {
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     // du over local positions q in [0, s*nP + k); the overhang beyond the tile becomes the new carry
     {
       const int fin = a.s * nP;
-      float* db = du + static_cast<size_t>(b) * a.L;
+      float* db = du + static_cast<size_t>(b) * a.pL;
       for (int q = tid; q < fin + a.k; q += NT) {
         float v = 0.f;
         for (int j = 0; j < a.k; ++j) {
@@ -748,7 +749,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
     for (int q = tid; q < a.k; q += NT) {
-      if (c == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = carry[par][bl][q];
+      if (c == a.n_chunks - 1) du[static_cast<size_t>(b) * a.pL + a.Lout + q] = carry[par][bl][q];
       else halo[(static_cast<size_t>(b) * a.n_chunks + c) * a.k + q] = carry[par][bl][q];
     }
     if (tid < a.H) dth_slab[(static_cast<size_t>(c) * a.B + b) * a.H + tid] = dth[bl][tid];
@@ -806,6 +807,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   KArgs a;
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.bn = d->bn; a.s = g.s; a.swap_out = d->swap_out;
+  a.pL = d->u_pitch ? d->u_pitch : d->L; a.pLo = d->out_pitch ? d->out_pitch : g.Lout;
   a.n_logsig = d->n_logsig; a.n_win = d->n_win; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks;
   a.S = g.S;
   a.KS = (d->k + 3) / 4;
@@ -900,7 +902,7 @@ int flow4_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, 
   VISSM_CHECK_LAUNCH("flow4_bwd");
   prof_end(VISSM_PROF_FLOW_BWD_DU, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, a.pL, d->k, g.n_chunks, g.s, g.CH, st);
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {

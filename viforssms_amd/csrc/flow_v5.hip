@@ -255,6 +255,7 @@ __host__ __device__ constexpr int n_frags(int NH, int KB, int JB) { return 16 * 
 
 struct KArgs {
   int B, L, k, H, s, swap_out, n_logsig, Lout, Lh, CH, n_chunks, S, n_groups, n_items;
+  int pL, pLo;  // row strides of u / du and u_next / du_next (VissmFlowDesc.u_pitch / out_pitch)
   int dc16;  // backward, bf16 products, one window: the dC slab holds bf16 partials (half the reduce's reads)
   int ncu;  // compute units of the device (the backward's wave priority pattern)
 };
@@ -732,8 +733,8 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(KArgs a, const float* __rest
   const int lwi = (win && lane < nb) ? win[b_lo + lane] : 0;
   for (int bl = 0; bl < nb; ++bl) {
     const int b = b_lo + bl;
-    const float* ub = u + static_cast<size_t>(b) * a.L;
-    float* ob = u_next + static_cast<size_t>(b) * a.Lout;
+    const float* ub = u + static_cast<size_t>(b) * a.pL;
+    float* ob = u_next + static_cast<size_t>(b) * a.pLo;
     const int wi = lane_i(lwi, bl);
     const float* Cw = C + static_cast<size_t>(wi) * a.Lh * HP;
     float ls = 0.f;
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
           fz_bp = fz.bin[wo];
         }
         Win<KB> wn;
-        fetch_win<KB>(a, u + static_cast<size_t>(b) * a.L, FZ ? nullptr : gout + static_cast<size_t>(b) * a.Lout, t0, wn);
+        fetch_win<KB>(a, u + static_cast<size_t>(b) * a.pL, FZ ? nullptr : gout + static_cast<size_t>(b) * a.pLo, t0, wn);
         load_ct(Cw, tht + static_cast<size_t>(b) * HP, m0, nZ, XN);
         stage_win<KB>(wn, uw, gw);
       }
@@ -1148,7 +1149,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
       if constexpr (DWL) dw_late();
       // du over local positions q in [0, fin + k): transposed conv + pass-through + carry
       if constexpr (DU) {
-        float* db = du + static_cast<size_t>(b) * a.L;
+        float* db = du + static_cast<size_t>(b) * a.pL;
         // fin + k <= 64 when PADDED (k <= 32), <= 96 otherwise
         constexpr int NBASE = PADDED ? 1 : 2;
         const int lim = fin + a.k;
@@ -1238,7 +1239,7 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
     const int b = b_lo + bl;
     for (int q = lane; q < a.k * wdu; q += 64) {
       const float v = mycarry[bl * KP + q];
-      if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
+      if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.pL + a.Lout + q] = v;
       else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
     }
     if (lane < a.H) dth_slab[(static_cast<size_t>(chn) * a.B + b) * a.H + lane] = dthl[w][bl][swz(lane)] * kLog2e;
@@ -1469,10 +1470,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         float uv[2], gv[2] = {0.f, 0.f};
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          const float* ub = u + static_cast<size_t>(bv[cb]) * a.L;
+          const float* ub = u + static_cast<size_t>(bv[cb]) * a.pL;
           uv[cb] = lane < nu ? ub[clampi(t0 + lane, a.L)] : 0.f;
           if constexpr (!FZ) {
-            if (lane < P) gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.Lout + clampi(t0 + lane, a.Lout)];
+            if (lane < P) gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.pLo + clampi(t0 + lane, a.Lout)];
           }
         }
         if (!two) gv[1] = 0.f;
@@ -1834,7 +1835,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           if (oq2 >= 0 && oq2 < nP) v += NPR == 2 ? gwin[w][cbq][oq2] : gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
           const int blq = cbq ? blv[1] : blv[0];
           if (q < a.k) v += carry[w][blq][q];
-          if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.L + t0 + q] = v;
+          if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.pL + t0 + q] = v;
           else carry[w][blq][q - nP] = v;
         }
       }
@@ -1881,7 +1882,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
     if constexpr (DU) {
       if (lane < a.k) {
         const float v = carry[w][bl][lane];
-        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + lane] = v;
+        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.pL + a.Lout + lane] = v;
         else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + lane] = v;
       }
     }
@@ -2015,7 +2016,7 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int i = 0; i < KB; ++i)
-            uv[cb][i] = 64 * i + lane < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + 64 * i + lane, a.L)] : 0.f;
+            uv[cb][i] = 64 * i + lane < nu ? u[static_cast<size_t>(bv[cb]) * a.pL + clampi(t0 + 64 * i + lane, a.L)] : 0.f;
         const f4* crow = reinterpret_cast<const f4*>(C + static_cast<size_t>(m0 + clampi(c, nP)) * HP) + g;
         f4 cr[4], tr[2][4];
 #pragma unroll
@@ -2103,7 +2104,7 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
           if (cb == 1 && !two) break;
           const float sg = softplus_fast(d[cb][1]) + 1e-10f;
           const int oq = ss * c + (ss - 1), o = t0 + oq;
-          float* ob = u_next + static_cast<size_t>(bv[cb]) * a.Lout;
+          float* ob = u_next + static_cast<size_t>(bv[cb]) * a.pLo;
           ob[swp ? (o ^ 1) : o] = uwin[w][cb][oq + a.k] * sg + d[cb][0];
           if (ss == 2) {  // the even outputs pass through (lotka_volterra_partial.py:97-104)
             const int oe = t0 + 2 * c;
@@ -2224,10 +2225,10 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
           for (int i = 0; i < UWN / 64; ++i)
-            uv[cb][i] = lane + 64 * i < nu ? u[static_cast<size_t>(bv[cb]) * a.L + clampi(t0 + lane + 64 * i, a.L)] : 0.f;
+            uv[cb][i] = lane + 64 * i < nu ? u[static_cast<size_t>(bv[cb]) * a.pL + clampi(t0 + lane + 64 * i, a.L)] : 0.f;
           if (lane < s * P) {
             const int o = t0 + lane;
-            gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.Lout + clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
+            gv[cb] = gout[static_cast<size_t>(bv[cb]) * a.pLo + clampi(a.swap_out ? (o ^ 1) : o, a.Lout)];
           }
         }
         if (!two) gv[1] = 0.f;
@@ -2537,7 +2538,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
             }
             const int blq = blv[cb];
             if (q < a.k) v += carry[w][blq][q];
-            if (q < fin) du[static_cast<size_t>(bv[cb]) * a.L + t0 + q] = v;
+            if (q < fin) du[static_cast<size_t>(bv[cb]) * a.pL + t0 + q] = v;
             else carry[w][blq][q - fin] = v;
           }
           }
@@ -2573,7 +2574,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
     if constexpr (DU) {
       for (int q = lane; q < a.k; q += 64) {
         const float v = carry[w][bl][q];
-        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.L + a.Lout + q] = v;
+        if (chn == a.n_chunks - 1) du[static_cast<size_t>(b) * a.pL + a.Lout + q] = v;
         else halo[(static_cast<size_t>(b) * a.n_chunks + chn) * a.k + q] = v;
       }
     }
@@ -2727,6 +2728,7 @@ static int device_cus() {
 static KArgs make_args(const VissmFlowDesc* d, const Geom& g) {
   KArgs a;
   a.B = d->B; a.L = d->L; a.k = d->k; a.H = d->H; a.s = g.s; a.swap_out = d->swap_out;
+  a.pL = d->u_pitch ? d->u_pitch : d->L; a.pLo = d->out_pitch ? d->out_pitch : g.Lout;
   a.n_logsig = d->n_logsig; a.Lout = g.Lout; a.Lh = g.Lh; a.CH = g.CH; a.n_chunks = g.n_chunks; a.S = g.S;
   a.n_groups = g.n_groups; a.n_items = g.n_items;
   a.dc16 = (d->n_win == 1 && d->precision != VISSM_PREC_FP32 && d->precision != VISSM_PREC_BF16X3) ? 1 : 0;
@@ -3021,7 +3023,7 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   VISSM_CHECK_LAUNCH("flow5_bwd");
   prof_end(pvar, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  int rc = du ? launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st) : VISSM_OK;
+  int rc = du ? launch_halo_fixup(du, ws.halo, d->B, d->L, a.pL, d->k, g.n_chunks, g.s, g.CH, st) : VISSM_OK;
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {
@@ -3117,7 +3119,7 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   VISSM_CHECK_LAUNCH("flow5_fused");
   prof_end(VISSM_PROF_FLOW_FUSED, st);
   prof_end(VISSM_PROF_FLOW_BWD, st);
-  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, d->k, g.n_chunks, g.s, g.CH, st);
+  int rc = launch_halo_fixup(du, ws.halo, d->B, d->L, a.pL, d->k, g.n_chunks, g.s, g.CH, st);
   if (rc) return rc;
   const int64_t nC = static_cast<int64_t>(g.Lh) * d->H;
   if (d->n_win == 1) {

@@ -33,7 +33,7 @@ float vissm_host_obs(float x, float y, float bin, float sd, float* gx) { return 
 // the last field}
 void vissm_host_abi_layout(int which, size_t* out) {
   switch (which) {
-    case 0: out[0] = sizeof(VissmFlowDesc); out[1] = offsetof(VissmFlowDesc, chunk_tiles); break;
+    case 0: out[0] = sizeof(VissmFlowDesc); out[1] = offsetof(VissmFlowDesc, out_pitch); break;
     case 1: out[0] = sizeof(VissmFlowParams); out[1] = offsetof(VissmFlowParams, theta_rank); break;
     default: out[0] = sizeof(VissmFlowGrads); out[1] = offsetof(VissmFlowGrads, b_head); break;
   }

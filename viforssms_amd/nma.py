@@ -360,6 +360,9 @@ class Engine:
         # tiles per t-chunk forced on every flow launch (VissmFlowDesc.chunk_tiles; 0 = automatic): parity tests
         # run a large batch's launch geometry at a small batch
         self.chunk_tiles = 0
+        # a flow output that feeds another flow is allocated with rows padded to 16 floats (FlowShape.pad_out), so
+        # that flow's du t-chunk stores are 64-byte aligned; VISSM_ROW_PAD=0 keeps dense rows (A/B)
+        self.pad_rows = os.environ.get("VISSM_ROW_PAD", "1") != "0"
         # data parallelism: a DistCtx here makes forward() route each flow's C and w_eps through
         # _SumGradOverRanks (set per step by VISSMBase when every rank holds the same windows)
         self.grad_sum = None
@@ -455,7 +458,7 @@ class Engine:
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
                               stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1),
                               n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
-                              chunk_tiles=self.chunk_tiles)
+                              chunk_tiles=self.chunk_tiles, pad_out=self.pad_rows and i < md.n_flows - 1)
             u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta), grad_sum=self.grad_sum)
             lq = lq - ls
             L -= md.k
@@ -545,7 +548,7 @@ class Engine:
             pf, pb = self.flow_precisions()
             shape = FlowShape(B=B, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn, stride2=False,
                               swap_out=False, n_logsig=md.n_logsig, n_win=batch.n_win, precision=pf, bwd_precision=pb,
-                              chunk_tiles=self.chunk_tiles)
+                              chunk_tiles=self.chunk_tiles, pad_out=self.pad_rows)
             u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta))
             lq = lq - ls
             L -= md.k
@@ -558,7 +561,7 @@ class Engine:
         scale = md.scale_num / md.M
         f = batch.feeds
         x, logsig, du, dC, dtt, gw = ar_last_flow_fused(
-            shape, batch.win, u.detach().contiguous(), C.detach(), tt.detach(), theta.detach().contiguous(), f.obs,
+            shape, batch.win, u.detach(), C.detach(), tt.detach(), theta.detach().contiguous(), f.obs,
             f.obs_bin, md.obs_std, scale, w_eps.detach(), w_hid.detach(), b_hid.detach(), w_head.detach(),
             b_head.detach(), self.theta_fold(fl, theta))
         # sde / obs from the written path and their theta gradient (x is a constant here: the fused kernel

@@ -35,6 +35,12 @@ def _require_gpu(*ts):
             raise _lib.VissmError("expected contiguous tensors")
 
 
+def _require_rows(*ts):
+    """As _require_gpu for [B, n] row tensors that may lie a pitch apart (VissmFlowDesc.u_pitch / out_pitch)."""
+    for t in ts:
+        _require_gpu(t[0] if t.dim() == 2 and t.stride(1) == 1 else t)   # one row: unit stride
+
+
 def _workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -140,10 +146,13 @@ class FlowShape:
     precision: int = _lib.VISSM_PREC_FP32
     bwd_precision: Optional[int] = None   # the backward kernel's precision when it differs (VISSM_PREC_BF16X3F)
     chunk_tiles: int = 0                  # VissmFlowDesc.chunk_tiles: 0 = automatic launch geometry
+    pad_out: bool = False                 # u_next rows padded to 16 floats (it feeds another flow, whose du stores
+                                          # are then 64-byte aligned)
 
-    def desc(self) -> FlowDesc:
+    def desc(self, u_pitch: int = 0, out_pitch: int = 0) -> FlowDesc:
         return FlowDesc(self.B, self.L, self.k, self.H, self.n_hidden, int(self.bn), int(self.stride2),
-                        int(self.swap_out), self.n_logsig, self.n_win, self.precision, int(self.chunk_tiles))
+                        int(self.swap_out), self.n_logsig, self.n_win, self.precision, int(self.chunk_tiles),
+                        int(u_pitch), int(out_pitch))
 
     @property
     def Lout(self):
@@ -230,10 +239,13 @@ class MAFlowFn(torch.autograd.Function):
     def forward(ctx, shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head,
                 tf=None):
         lib = _lib.load()
-        _require_gpu(u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, win)
+        u = _rows(u, shape.L)
+        _require_rows(u)
+        _require_gpu(C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, win)
         dev = u.device
-        d = shape.desc()
-        u_next = torch.empty(shape.B, shape.Lout, dtype=torch.float32, device=dev)
+        pout = (shape.Lout + 15) // 16 * 16 if shape.pad_out else shape.Lout
+        d = shape.desc(_pitch(u, shape.L), pout)
+        u_next = _rows_empty(shape.B, shape.Lout, pout, dev)
         logsig = torch.empty(shape.B, dtype=torch.float32, device=dev)
         wsz = lib.vissm_flow_workspace_size(ctypes.byref(d), 0)
         if wsz == 0:
@@ -263,14 +275,16 @@ class MAFlowFn(torch.autograd.Function):
             g_next = torch.zeros(shape.B, shape.Lout, dtype=torch.float32, device=dev)
         if g_ls is None:
             g_ls = torch.zeros(shape.B, dtype=torch.float32, device=dev)
-        g_next = g_next.contiguous()
+        g_next = _rows(g_next, shape.Lout)
         g_ls = g_ls.contiguous()
         if shape.bwd_precision is not None:
             shape = dataclasses.replace(shape, precision=shape.bwd_precision, bwd_precision=None)
-        d = shape.desc()
+        u = _rows(u, shape.L)
+        pu = _pitch(u, shape.L)
+        d = shape.desc(pu, _pitch(g_next, shape.Lout))
         # the base noise needs no gradient: the bf16 kernels then skip the transposed convolution
         need_du = ctx.needs_input_grad[2] or shape.precision == _lib.VISSM_PREC_FP32 or _FORCE_DU
-        du = torch.empty_like(u) if need_du else None
+        du = _rows_empty(shape.B, shape.L, pu, dev) if need_du else None   # du rows at u's pitch
         dC = torch.empty_like(C)
         dth = torch.empty_like(theta_term)
         gw = [torch.empty_like(t) if t is not None else None for t in (w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head)]
@@ -282,6 +296,24 @@ class MAFlowFn(torch.autograd.Function):
                                  ptr(g_next), ptr(g_ls), ptr(du), ptr(dC), ptr(dth), ctypes.byref(grads), ptr(ws),
                                  wsz, _lib.stream_handle(dev)), "vissm_flow_bwd")
         return (None, None, du, dC, dth, *gw, None)
+
+
+def _rows(t: torch.Tensor, n: int) -> torch.Tensor:
+    """t as rows of n unit-stride floats at some pitch >= n (VissmFlowDesc.u_pitch / out_pitch); copied only when it
+    is not (a transposed or sliced-column view)."""
+    if t.stride(1) != 1 or (t.shape[0] > 1 and t.stride(0) < n):
+        t = t.contiguous()
+    return t
+
+
+def _pitch(t: torch.Tensor, n: int) -> int:
+    return t.stride(0) if t.shape[0] > 1 else n
+
+
+def _rows_empty(B: int, n: int, pitch: int, device) -> torch.Tensor:
+    """[B, n] float32 rows `pitch` floats apart (a column slice of a [B, pitch] buffer)."""
+    buf = torch.empty(B, pitch, dtype=torch.float32, device=device)
+    return buf if pitch == n else buf[:, :n]
 
 
 def ma_flow(shape: FlowShape, win, u, C, theta_term, w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf=None):
@@ -301,16 +333,19 @@ def ar_last_flow_fused(shape: FlowShape, win, u, C, theta_term, theta, obs, obs_
     through vissm_elbo_bwd on x).  Returns (x [B, Lout], logsig [B], du, dC, dtheta_term,
     [g_w_eps, g_w_hid, g_b_hid, g_w_head, g_b_head])."""
     lib = _lib.load()
-    _require_gpu(u, C, theta_term, theta, obs, obs_bin, w_eps, w_hid, b_hid, w_head, b_head, win)
+    u = _rows(u, shape.L)
+    _require_rows(u)
+    _require_gpu(C, theta_term, theta, obs, obs_bin, w_eps, w_hid, b_hid, w_head, b_head, win)
     dev = u.device
-    d = shape.desc()
+    pu = _pitch(u, shape.L)
+    d = shape.desc(pu, 0)
     wsz = lib.vissm_flow_ar_elbo_fused_workspace_size(ctypes.byref(d))
     if wsz == 0:
         raise _lib.VissmError("vissm_flow_ar_elbo_fused: unsupported flow shape")
     ws = _workspace(wsz, dev)
     x = torch.empty(shape.B, shape.Lout, dtype=torch.float32, device=dev)
     logsig = torch.empty(shape.B, dtype=torch.float32, device=dev)
-    du = torch.empty_like(u)
+    du = _rows_empty(shape.B, shape.L, pu, dev)
     dC = torch.empty_like(C)
     dth = torch.empty_like(theta_term)
     gw = [torch.empty_like(t) for t in (w_eps, w_hid, b_hid, w_head, b_head)]
