@@ -99,6 +99,20 @@ def test_flow_geometry_forced_chunk_tiles():
         _lib.flow_geometry(d, 1)
 
 
+def test_flow_row_pitch_validates_without_gpu():
+    """VissmFlowDesc.u_pitch / out_pitch (0 = dense) must cover the row: a pitch below L (L - k) is rejected before
+    any launch; the fused last flow writes x dense (out_pitch 0 or L - k only)."""
+    from viforssms_amd import _lib
+    from viforssms_amd.ops import FlowShape
+    lib = _lib.load()
+    sh = FlowShape(B=4, L=5017, k=8, H=50, n_hidden=1, bn=False, stride2=False, swap_out=False, n_logsig=5000, n_win=1,
+                   precision=_lib.VISSM_PREC_BF16)
+    for up, op, ok in [(0, 0, True), (5024, 5024, True), (5017, 5009, True), (5016, 0, False), (0, 5008, False)]:
+        d = sh.desc(up, op)
+        assert (lib.vissm_flow_workspace_size(ctypes.byref(d), 1) > 0) == ok, (up, op)
+    assert lib.vissm_flow_ar_elbo_fused_workspace_size(ctypes.byref(sh.desc(5024, 0))) > 0
+
+
 def _host():
     lib = ctypes.CDLL(HOSTCHECK)
     f = lib.vissm_host_trans
