@@ -461,7 +461,9 @@ def measure(args, ctx, dev, parity_line: bool):
     # states (libvissm records them with its HIP events: z read / dz written by the log-density kernels,
     # eps written by the base-noise kernel) over the live launch time, against the 8 TB/s HBM peak
     fused = bool(prof[_lib.PROF_FLOW_FUSED][1])
-    names = {_lib.PROF_ELBO_FWD: "elbo_fwd_kernel (log-densities: reads z)",
+    names = {_lib.PROF_ELBO_FWD: ("elbo_fwd_kernel (reads z: the log-densities and their per-sample theta gradient in "
+                                  "one pass, vissm_elbo_fwd_theta_grad)") if fused else
+                                 "elbo_fwd_kernel (log-densities: reads z)",
              _lib.PROF_ELBO_BWD: ("elbo_bwd_kernel (reads z, writes the per-sample theta gradient only: the fused "
                                   "last flow differentiated through z itself)") if fused else
                                  "elbo_bwd_kernel (reads z, writes dz)",

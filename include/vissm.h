@@ -231,6 +231,15 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data,
                    const float* g_obs, const float* g_extra, float* dz,
                    float* dtheta, void* stream);
 
+/* vissm_elbo_fwd and the theta gradient of vissm_elbo_bwd with dz = NULL, for a path z that is a
+ * constant (the training step after vissm_flow_ar_elbo_fused): sde, obs (and extra) per sample and
+ * dtheta = d(g_sde . sde + g_obs . obs + g_extra . extra)/dtheta.  AR(1): one pass over z (the two calls
+ * would read it twice); other models: the two calls.  Same reference terms as vissm_elbo_fwd. */
+int vissm_elbo_fwd_theta_grad(const VissmElboDesc* d, const VissmElboData* data, const float* z,
+                              const float* theta, const float* g_sde, const float* g_obs,
+                              const float* g_extra, float* sde, float* obs, float* extra,
+                              float* dtheta, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Global-norm clip + Adamax over one flat parameter buffer:
  * tf.global_norm / tf.clip_by_global_norm (AR.py:230-232) followed by

@@ -75,3 +75,31 @@ def test_ar_elbo_bwd_without_obs_gradient():
     (sde * gs.float().to(DEV)).sum().backward()
     np.testing.assert_allclose(zd.grad.double().cpu().numpy(), zr.grad.numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(thd.grad.double().cpu().numpy(), thr.grad.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [1, 3, 4, 9, 1001, 5000])
+@pytest.mark.parametrize("n_win", [1, 3])
+def test_ar_elbo_values_and_theta_grad_one_pass(M, n_win):
+    """vissm_elbo_fwd_theta_grad (the fused training step's one pass over x): sde / obs agree with vissm_elbo_fwd
+    (to fp32 rounding) and the theta gradient matches the float64 oracle's d(gs . sde)/d theta (z constant) like
+    vissm_elbo_bwd's."""
+    from viforssms_amd import _lib
+    from viforssms_amd.ops import ElboFeeds, elbo_terms, elbo_values_and_theta_grad
+    B, obs_std = 37, 1.3
+    z, theta, obs, obs_bin, win, gs, go = _case(B, M, n_win, seed=M * 5 + n_win)
+    thr = theta.clone().requires_grad_(True)
+    wl = win.long()
+    sde_r, obs_r = O.ar_elbo_terms(z, thr, obs[wl], obs_bin[wl], obs_std)
+    (sde_r * gs + obs_r * go).sum().backward()
+    feeds = ElboFeeds(obs=obs.float().to(DEV), obs_bin=obs_bin.float().to(DEV),
+                      win=win.to(DEV) if n_win > 1 else None, n_win=n_win)
+    zd, thd = z.float().to(DEV), theta.float().to(DEV)
+    sde, obs_lp, dth = elbo_values_and_theta_grad(_lib.MODEL_AR, M, 1.0, obs_std, feeds, zd, thd,
+                                                  gs.float().to(DEV), go.float().to(DEV))
+    sde2, obs2, _ = elbo_terms(_lib.MODEL_AR, M, 1.0, obs_std, feeds, zd, thd)
+    torch.cuda.synchronize()
+    rel = lambda a, b: float((a.double().cpu() - b.double().cpu()).norm() / (b.double().norm() + 1e-30))
+    # the same sums as vissm_elbo_fwd (the extra theta sums change the compiler's FMA contraction: an ulp or so)
+    assert rel(sde, sde2) < 1e-6 and rel(obs_lp, obs2) < 1e-6
+    assert rel(sde, sde_r.detach()) < 1e-5 and rel(obs_lp, obs_r.detach()) < 1e-5
+    assert rel(dth, thr.grad) < 1e-5, rel(dth, thr.grad)

@@ -598,9 +598,13 @@ __device__ __forceinline__ f4u ldz4(const float* p) {
   return ld4(p);
 }
 
+// TG (vissm_elbo_fwd_theta_grad): the same pass also sums z_t and z_t x_t for d(g_sde sde)/d theta (z constant):
+// d/dth0 = g is sum z, d/dth1 = g is sum z x_t, d/dth2 = g (sum z^2 - M) -- the terms ar_elbo_bwd_kernel sums
+template <bool TG>
 __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* __restrict__ z,
                                                           const float* __restrict__ theta, float* __restrict__ sde,
-                                                          float* __restrict__ obs) {
+                                                          float* __restrict__ obs, const float* __restrict__ g_sde,
+                                                          float* __restrict__ dtheta) {
   const int lane = threadIdx.x & 63;
   const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kArW + (threadIdx.x >> 6));
   if (b >= a.B) return;  // wave-uniform
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
   const float* bb = a.d.obs_bin + static_cast<size_t>(w) * M;
   const float th0 = theta[b * 3 + 0], th1 = theta[b * 3 + 1], th2 = theta[b * 3 + 2];
   const float is = __expf(-th2), io = 1.f / a.obs_std;
-  float sq = 0.f, so = 0.f, sb = 0.f;
+  float sq = 0.f, so = 0.f, sb = 0.f, s0 = 0.f, s1 = 0.f;
   auto chunk = [&](const f4u& x, float xn, const f4u& y, const f4u& bn) {
     const float xs[kArV + 1] = {x[0], x[1], x[2], x[3], xn};
 #pragma unroll
@@ -621,6 +625,10 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
       sq += zt * zt;
       so += bn[j] * zo * zo;
       sb += bn[j];
+      if constexpr (TG) {
+        s0 += zt;
+        s1 += zt * xs[j];
+      }
     }
   };
   // transitions t -> t+1, t in [0, M): full chunks of V (kArU per lane at a time), then the tail
@@ -650,10 +658,24 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
     sq += zt * zt;
     so += bb[t] * zo * zo;
     sb += bb[t];
+    if constexpr (TG) {
+      s0 += zt;
+      s1 += zt * zb[t];
+    }
   }
   const double rq = wave_sum(static_cast<double>(sq));
   const double ro = wave_sum(static_cast<double>(so));
   const double rb = wave_sum(static_cast<double>(sb));
+  if constexpr (TG) {
+    const double r0 = wave_sum(static_cast<double>(s0));
+    const double r1 = wave_sum(static_cast<double>(s1));
+    if (lane == 0) {
+      const float gs = g_sde ? g_sde[b] : 0.f;
+      dtheta[b * 3 + 0] = static_cast<float>(gs * is * r0);
+      dtheta[b * 3 + 1] = static_cast<float>(gs * is * r1);
+      dtheta[b * 3 + 2] = static_cast<float>(gs * (rq - M));
+    }
+  }
   if (lane == 0) {
     sde[b] = static_cast<float>(-0.5 * rq + M * (-static_cast<double>(th2) - 0.5 * kLog2Pi));
     if (obs) obs[b] = static_cast<float>(-0.5 * ro + rb * (-std::log(static_cast<double>(a.obs_std)) - 0.5 * kLog2Pi));
@@ -812,7 +834,10 @@ int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   dim3 grid((d->B + kSW - 1) / kSW), blk(256);
   prof_begin(VISSM_PROF_ELBO_FWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_fwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, sde, obs); break;
+    case VISSM_MODEL_AR:
+      hipLaunchKernelGGL(ar_elbo_fwd_kernel<false>, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, sde, obs,
+                         nullptr, nullptr);
+      break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
     default: hipLaunchKernelGGL(stream_fwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, sde, obs, extra); break;
@@ -845,6 +870,27 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   // algorithmic bytes: z read, dz written, theta / dtheta and the upstream gradients
   prof_end(VISSM_PROF_ELBO_BWD, st,
            4.0 * d->B * ((dz ? 2.0 : 1.0) * zlen_of(d) + 2 * theta_len(d->model) + 3));
+  return VISSM_OK;
+}
+
+int vissm_elbo_fwd_theta_grad(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta,
+                              const float* g_sde, const float* g_obs, const float* g_extra, float* sde, float* obs,
+                              float* extra, float* dtheta, void* stream) {
+  if (!d || d->model != VISSM_MODEL_AR) {
+    const int rc = vissm_elbo_fwd(d, data, z, theta, sde, obs, extra, stream);
+    return rc ? rc : vissm_elbo_bwd(d, data, z, theta, g_sde, g_obs, g_extra, nullptr, dtheta, stream);
+  }
+  int rc = check(d, data);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(z && theta && sde && dtheta, "elbo_fwd_theta_grad: null pointer");
+  if (d->B == 0) return VISSM_OK;
+  Args a = make(d, data);
+  hipStream_t st = as_stream(stream);
+  prof_begin(VISSM_PROF_ELBO_FWD, st);
+  hipLaunchKernelGGL(ar_elbo_fwd_kernel<true>, dim3((d->B + kArW - 1) / kArW), dim3(256), 0, st, a, z, theta, sde, obs,
+                     g_sde, dtheta);
+  VISSM_CHECK_LAUNCH("elbo_fwd_theta_grad");
+  prof_end(VISSM_PROF_ELBO_FWD, st, 4.0 * d->B * (static_cast<double>(zlen_of(d)) + 2 * theta_len(d->model) + 4));
   return VISSM_OK;
 }
 

@@ -438,12 +438,18 @@ def elbo_values_and_theta_grad(model: int, M: int, dt: float, obs_std: float, fe
     sde = torch.empty(B, dtype=torch.float32, device=z.device)
     obs = torch.empty_like(sde)
     extra = torch.empty_like(sde)
-    st = _lib.stream_handle(z.device)
-    check(lib.vissm_elbo_fwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(sde), ptr(obs), ptr(extra),
-                             st), "vissm_elbo_fwd")
     dth = torch.empty_like(theta)
-    check(lib.vissm_elbo_bwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde), ptr(g_obs),
-                             ptr(extra), None, ptr(dth), st), "vissm_elbo_bwd")
+    st = _lib.stream_handle(z.device)
+    if os.environ.get("VISSM_ELBO_TWO_PASS") == "1":   # A/B hook: the two calls, z read twice
+        check(lib.vissm_elbo_fwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(sde), ptr(obs),
+                                 ptr(extra), st), "vissm_elbo_fwd")
+        check(lib.vissm_elbo_bwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde), ptr(g_obs),
+                                 ptr(extra), None, ptr(dth), st), "vissm_elbo_bwd")
+        return sde, obs, dth
+    # one pass over z for AR(1) (vissm_elbo_fwd then vissm_elbo_bwd with dz = NULL for the other models)
+    check(lib.vissm_elbo_fwd_theta_grad(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde),
+                                        ptr(g_obs), ptr(extra), ptr(sde), ptr(obs), ptr(extra), ptr(dth), st),
+          "vissm_elbo_fwd_theta_grad")
     return sde, obs, dth
 
 
