@@ -260,7 +260,8 @@ def build_model(args, ctx, dev, prec):
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (default: the launcher's WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", choices=["ar", "lv", "sv", "fhn"], default="ar",
@@ -535,9 +536,10 @@ def main():
 
     # --gpus N without torchrun: launch N ranks (torchrun, 127.0.0.1) from here before any GPU call and exit with
     # their status; under torchrun the world must be N
-    rc = ensure_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
-    if rc is not None:
-        sys.exit(rc)
+    if args.gpus is not None:
+        rc = ensure_world(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+        if rc is not None:
+            sys.exit(rc)
 
     ctx = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -54,6 +54,11 @@ extern "C" {
 
 const char* vissm_last_error(void);
 int vissm_version(void);
+/* sha256 (hex) of the sources the library was built from (viforssms_amd/srchash.py); the Python host refuses a
+ * library whose hash differs from its source tree.  vissm_build_flags: extra compile flags of an A/B build ("" for
+ * the production build). */
+const char* vissm_source_hash(void);
+const char* vissm_build_flags(void);
 
 /* ---------------------------------------------------------------------------
  * Base noise: init_dist.slp (AR.py:24-35; lotka_volterra_partial.py:25-36).
@@ -146,6 +151,12 @@ size_t vissm_flow_workspace_size(const VissmFlowDesc* d, int32_t backward);
  * equivalent (TF1 has no launch geometry): the parity tests read it at a benchmark batch and pass
  * out[1] as chunk_tiles at a small one. */
 int vissm_flow_geometry(const VissmFlowDesc* d, int32_t which, int32_t* out);
+
+/* The precision vissm_flow_fwd / vissm_flow_bwd compute a descriptor in: its own where the matrix-core kernels cover
+ * the shape, VISSM_PREC_FP32 where the call falls back to the exact-fp32 kernels (bf16 / bf16x3 / bf16x2 requests
+ * beyond flow5's shapes: never less precise than asked; du must then be non-NULL).  Host arithmetic, no GPU;
+ * VISSM_EINVAL for an invalid descriptor or VISSM_PREC_BF16X2_BF16 (a fused-flow precision). */
+int32_t vissm_flow_kernel_precision(const VissmFlowDesc* d);
 
 int vissm_flow_fwd(const VissmFlowDesc* d, const VissmFlowParams* w,
                    const float* u, const float* C, const int32_t* win,

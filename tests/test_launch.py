@@ -41,3 +41,29 @@ def test_plain_python_gpus_2_spawns_two_ranks(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     got = sorted(open(tmp_path / f).read().split() for f in os.listdir(tmp_path))
     assert got == [["0", "2", "2"], ["1", "2", "2"]]
+
+
+def test_launcher_never_touches_the_gpu_runtime(monkeypatch):
+    """The parent that spawns the ranks must not initialise HIP (a GPU-initialised process must not start the
+    ranks): ensure_world counts devices from the visibility variables / render nodes, never through torch.cuda."""
+    import torch
+
+    def _boom(*a, **k):
+        raise AssertionError("the launcher queried the GPU runtime")
+
+    for v in DIST_VARS:
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", _boom)
+    monkeypatch.setattr(torch.cuda, "is_available", _boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", _boom, raising=False)
+    calls = []
+    monkeypatch.setattr(launch.subprocess, "call", lambda cmd: calls.append(cmd) or 0)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert launch.ensure_world(2, "b.py", ["--gpus", "2"]) == 0
+    assert len(calls) == 1 and "--nproc-per-node=2" in calls[0]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    with pytest.raises(SystemExit, match="needs 2 visible GPUs"):
+        launch.ensure_world(2, "b.py", [])
+    monkeypatch.setenv("VISSM_DIST_BACKEND", "gloo")            # the one-GPU rehearsal may oversubscribe
+    assert launch.ensure_world(2, "b.py", []) == 0
+    assert not torch.cuda.is_initialized()

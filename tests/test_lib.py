@@ -33,6 +33,24 @@ def test_library_loads_and_exports_all_symbols():
     assert lib.vissm_version() >= 1
 
 
+def test_library_built_from_this_tree():
+    """The pushed binary is the built one: the source hash compiled into libvissm.so equals the hash of csrc/ +
+    include/vissm.h + the Makefile as they are now (fails when the .so is older than, or other than, the sources)."""
+    from viforssms_amd import _lib, srchash
+    lib = _lib.load()
+    assert lib.vissm_source_hash().decode() == srchash.source_hash()
+    assert lib.vissm_build_flags() == b"", "an A/B variant build is installed as the production library"
+    assert "viforssms_amd/csrc/flow_v5.hip" in srchash.source_files()
+
+
+def test_loader_refuses_foreign_library(monkeypatch):
+    from viforssms_amd import _lib, srchash
+    lib = _lib.load()
+    monkeypatch.setattr(srchash, "source_hash", lambda root=None: "0" * 64)
+    with pytest.raises(_lib.VissmError, match="built from other sources"):
+        _lib.check_source_hash(lib)
+
+
 def test_library_rejects_bad_shapes_without_gpu():
     from viforssms_amd import _lib
     lib = _lib.load()
@@ -274,3 +292,33 @@ def test_agpr_audit_detects_unpadded_reads(tmp_path):
     assert subprocess.run([sys.executable, script, str(bad)], capture_output=True).returncode == 1
     assert subprocess.run([sys.executable, script, str(good)], capture_output=True).returncode == 0
     assert subprocess.run([sys.executable, script, str(far)], capture_output=True).returncode == 0
+
+
+def test_flow_kernel_precision_query():
+    """vissm_flow_kernel_precision: bf16 / bf16x3 / bf16x2 run as asked on the shapes flow5 covers and fall back to
+    the exact-fp32 kernels elsewhere (k > 32 at one hidden layer; bf16x2 / bf16x3 at three hidden layers)."""
+    from viforssms_amd import _lib
+    from viforssms_amd.ops import FlowShape, kernel_precision
+    ar = dict(B=4, L=40, k=8, H=50, n_hidden=1, bn=False, stride2=False, swap_out=False, n_logsig=24, n_win=1)
+    lv = dict(B=4, L=40, k=4, H=50, n_hidden=3, bn=True, stride2=True, swap_out=True, n_logsig=24, n_win=1)
+    for prec in (_lib.VISSM_PREC_FP32, _lib.VISSM_PREC_BF16, _lib.VISSM_PREC_BF16X3, _lib.VISSM_PREC_BF16X2):
+        assert kernel_precision(FlowShape(**ar, precision=prec)) == prec
+    k50 = dict(ar, k=50, L=80)
+    assert kernel_precision(FlowShape(**k50, precision=_lib.VISSM_PREC_BF16X2)) == _lib.VISSM_PREC_FP32
+    assert kernel_precision(FlowShape(**k50, precision=_lib.VISSM_PREC_BF16)) == _lib.VISSM_PREC_BF16
+    assert kernel_precision(FlowShape(**lv, precision=_lib.VISSM_PREC_BF16)) == _lib.VISSM_PREC_BF16
+    assert kernel_precision(FlowShape(**lv, precision=_lib.VISSM_PREC_BF16X2)) == _lib.VISSM_PREC_FP32
+    with pytest.raises(_lib.VissmError):
+        kernel_precision(FlowShape(**ar, precision=_lib.VISSM_PREC_BF16X2_BF16))
+
+
+@pytest.mark.parametrize("family,k", [("lv", 4), ("ar", 50)])
+@pytest.mark.parametrize("prec", ["bf16x2", "bf16x2f"])
+def test_engine_refuses_bf16x2_beyond_split_kernels(family, k, prec):
+    """bf16x2 on LV / SV / FHN or AR with k > 32 used to run an fp32 forward under the bf16x2 label and
+    then stop in the first backward (du = NULL on the fp32 kernels); the engine now refuses it up front."""
+    from tests.parity_util import build_model
+    from viforssms_amd import _lib
+    with pytest.raises(ValueError, match="bf16x2"):
+        build_model(family, 4, 24, k, 2, 16, 5 if family == "lv" else 3, 3, "cpu",
+                    precision=_lib.TRAIN_PRECISIONS[prec])

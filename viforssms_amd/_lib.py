@@ -91,6 +91,8 @@ class ElboData(ctypes.Structure):
 SIGNATURES = {
     "vissm_last_error": (ctypes.c_char_p, []),
     "vissm_version": (_i32, []),
+    "vissm_source_hash": (ctypes.c_char_p, []),
+    "vissm_build_flags": (ctypes.c_char_p, []),
     "vissm_normal_base": (_i32, [_u64, _u64, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_normal_base_dev": (_i32, [_u64, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
     "vissm_base_logprob": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p]),
@@ -101,6 +103,7 @@ SIGNATURES = {
     "vissm_flow_bwd": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                               ctypes.POINTER(FlowGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_flow_kernel_precision": (_i32, [ctypes.POINTER(FlowDesc)]),
     "vissm_flow_ar_elbo_fused_supported": (_i32, [ctypes.POINTER(FlowDesc)]),
     "vissm_flow_ar_elbo_fused_workspace_size": (_size_t, [ctypes.POINTER(FlowDesc)]),
     "vissm_flow_ar_elbo_fused": (_i32, [ctypes.POINTER(FlowDesc), ctypes.POINTER(FlowParams), _c_void_p, _c_void_p,
@@ -164,8 +167,22 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    check_source_hash(lib, path)
     _lib = lib
     return lib
+
+
+def check_source_hash(lib: ctypes.CDLL, path: str = LIB_PATH) -> str:
+    """Refuse a library that was not built from this tree's sources (a stale or foreign `.so`): the hash compiled
+    into it (vissm_source_hash, Makefile) must equal srchash.source_hash() of the sources next to this module."""
+    from . import srchash
+    built = lib.vissm_source_hash().decode()
+    want = srchash.source_hash()
+    if built != want:
+        raise VissmError(
+            f"{path} was built from other sources (library {built[:16]}, tree {want[:16]}): rebuild it with "
+            "`make -C viforssms_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    return built
 
 
 def check(rc: int, what: str):

@@ -396,6 +396,9 @@ static int make(const VissmFeatDesc* d, Args* a) {
   a->Lh = d->Lh;
   VISSM_CHECK_ARG(d->Lh >= 1 && d->stride * (d->Lh - 1) + d->k <= d->Lf, "feat: Lh = %d needs s (Lh - 1) + k <= Lf = %d",
                   d->Lh, d->Lf);
+  // a forward block computes s (kT - 1) + k rows and the backward reads its s kT own rows: k >= s keeps every row the
+  // backward reads written by some forward block (k < s would leave row s kT - 1 of each block unwritten)
+  VISSM_CHECK_ARG(d->k >= d->stride, "feat: kernel_len %d < stride %d", d->k, d->stride);
   a->Lu = d->stride * (d->Lh - 1) + d->k;
   a->in_ws = d->in_win_stride;
   VISSM_CHECK_ARG(a->in_ws >= static_cast<int64_t>(d->Lf) * d->Cin || d->n_win == 1,

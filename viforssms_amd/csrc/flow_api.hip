@@ -166,6 +166,11 @@ int vissm_flow_bwd(const VissmFlowDesc* d, const VissmFlowParams* w, const float
   return flow2_bwd(d, w, u, C, win, theta_term, du_next, dlogsig, du, dC, dtheta_term, gr, workspace, ws_bytes, st);
 }
 
+int32_t vissm_flow_kernel_precision(const VissmFlowDesc* d) {
+  if (validate(d) != VISSM_OK || d->precision == VISSM_PREC_BF16X2_BF16) return VISSM_EINVAL;
+  return use_v5(d) ? d->precision : VISSM_PREC_FP32;
+}
+
 int32_t vissm_flow_ar_elbo_fused_supported(const VissmFlowDesc* d) {
   return (validate(d) == VISSM_OK && flow5_ar_fused_supports(d)) ? 1 : 0;
 }

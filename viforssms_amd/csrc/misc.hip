@@ -8,6 +8,13 @@
 #include <mutex>
 #include <vector>
 
+#ifndef VISSM_SRC_HASH
+#error "build through the Makefile: it defines VISSM_SRC_HASH (the source hash _lib.load() checks)"
+#endif
+#ifndef VISSM_BUILD_FLAGS
+#define VISSM_BUILD_FLAGS ""
+#endif
+
 namespace vissm {
 
 static thread_local char g_err[512] = "";
@@ -377,6 +384,8 @@ extern "C" {
 
 const char* vissm_last_error(void) { return vissm::g_err; }
 int vissm_version(void) { return 1; }
+const char* vissm_source_hash(void) { return VISSM_SRC_HASH; }
+const char* vissm_build_flags(void) { return VISSM_BUILD_FLAGS; }
 
 int vissm_normal_base(uint64_t seed, uint64_t offset, float* eps, float* base_lp, int32_t B, int32_t L,
                       int32_t n_last, void* stream) {

@@ -2,6 +2,7 @@
 RCCL ("nccl" backend on ROCm) when launched by torchrun, gloo on CPU-only hosts."""
 from __future__ import annotations
 
+import glob
 import os
 import socket
 import subprocess
@@ -17,6 +18,18 @@ def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process could hand to its ranks, WITHOUT touching the GPU runtime (torch.cuda.device_count() may
+    initialise HIP on this torch build, and a launcher must not spawn its ranks from a process that did): the
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list when one is set, else the DRM render
+    nodes.  0 = unknown."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    return len(glob.glob("/dev/dri/renderD*"))
 
 
 def rank_launch_cmd(gpus: int, script: str, argv: List[str], port: Optional[int] = None) -> List[str]:
@@ -40,7 +53,7 @@ def ensure_world(gpus: int, script: str, argv: List[str]) -> Optional[int]:
         return None
     if gpus == 1:
         return None
-    n_dev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    n_dev = visible_gpu_count()   # no torch.cuda here: the ranks are spawned from this process
     backend = os.environ.get("VISSM_DIST_BACKEND", "nccl")
     if 0 < n_dev < gpus and backend != "gloo":
         raise SystemExit(f"--gpus {gpus} needs {gpus} visible GPUs for RCCL, found {n_dev} "

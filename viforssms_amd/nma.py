@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import (FlowShape, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
+from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
                   ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
@@ -68,7 +68,14 @@ class _SumGradOverRanks(torch.autograd.Function):
     on the window-shared conv output C (and the sample-channel slice of the same conv kernel) when every rank
     holds the same windows: the window-shared backward (feature MLP, conv over features -- LV's 31.8 M
     parameters) is linear in dC, so running it replicated on the summed dC gives every rank the full-batch
-    gradient of those parameters with a [n_win, Lh, H] all-reduce per flow instead of theirs (vi_ssm.py)."""
+    gradient of those parameters with a [n_win, Lh, H] all-reduce per flow instead of theirs (vi_ssm.py).
+
+    Ordering invariant (RCCL needs the same collective sequence on every rank): these blocking all-reduces run
+    inside the autograd backward, interleaved with the per-flow bucket all-reduces VISSMBase launches from
+    post-accumulate hooks.  Both are issued in the order autograd visits the nodes, which is a function of the graph
+    alone; every rank builds the same graph (same model, same window plan -- the plan is only taken when all ranks
+    hold the same windows -- and the same per-rank batch shape), so the sequence agrees.  A rank-dependent graph
+    (e.g. a different flow count or a branch on local data) would break it."""
 
     @staticmethod
     def forward(ctx, x, dist_ctx):
@@ -224,7 +231,8 @@ class IAF:
         VISSM_FEAT_TORCH=1 selects the torch form everywhere, VISSM_FEAT_MAX_K moves the kernel_len bound (A/B timing)."""
         f = self.spec.feat
         kmax = int(os.environ.get("VISSM_FEAT_MAX_K", "16"))
-        if ts.is_cuda and f == "mlp4" and self.spec.k <= kmax and os.environ.get("VISSM_FEAT_TORCH") != "1":
+        if (ts.is_cuda and f == "mlp4" and s <= self.spec.k <= kmax
+                and os.environ.get("VISSM_FEAT_TORCH") != "1"):   # vissm_feat_* need kernel_len >= stride
             p = self._p
             return feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
                              p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
@@ -387,6 +395,27 @@ class Engine:
         self.theta_dist = ThetaFlow(self.store, mdef.P_theta, mdef.n_maf, self.perms, mdef.theta_base[0],
                                     mdef.theta_base[1], mdef.theta_act, rng)
         self.store.finalize(self.device)
+        self._check_precision()
+
+    def _check_precision(self):
+        """bf16x2 / bf16x2f are throughput modes of the split-weight matrix-core kernels (one hidden layer, k <= 32:
+        the AR configurations).  Elsewhere the flow calls would fall back to the exact-fp32 kernels and the mode's
+        name would misstate what ran, so the engine refuses it up front (vissm_flow_kernel_precision)."""
+        if self.precision not in (_lib.VISSM_PREC_BF16X2, _lib.VISSM_PREC_BF16X2F):
+            return
+        md = self.mdef
+        s = 2 if md.D == 2 else 1
+        L = md.kernel_ext
+        for i, fl in enumerate(self.flows):
+            shape = FlowShape(B=1, L=L, k=md.k, H=fl.spec.H, n_hidden=fl.spec.n_hidden, bn=fl.spec.bn,
+                              stride2=(s == 2), swap_out=(md.D == 2 and i < md.n_flows - 1), n_logsig=md.n_logsig,
+                              n_win=1, precision=_lib.VISSM_PREC_BF16X2)
+            if kernel_precision(shape) != _lib.VISSM_PREC_BF16X2:
+                raise ValueError(
+                    f"precision bf16x2 / bf16x2f runs on the split-weight matrix-core kernels only (one hidden layer, "
+                    f"kernel_len <= 32); {md.family} with {fl.spec.n_hidden} hidden layers and kernel_len {md.k} "
+                    "is not covered: use fp32, bf16 or bf16x3")
+            L -= md.k
 
     # ---- batches ----
     def make_batch(self, starts: np.ndarray) -> Batch:

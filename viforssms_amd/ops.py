@@ -163,6 +163,15 @@ class FlowShape:
         return self.Lout // (2 if self.stride2 else 1)
 
 
+def kernel_precision(shape: FlowShape) -> int:
+    """vissm_flow_kernel_precision: the precision the flow kernels compute `shape` in (its own, or fp32 where the
+    matrix-core kernels do not cover it)."""
+    rc = _lib.load().vissm_flow_kernel_precision(ctypes.byref(shape.desc()))
+    if rc < 0:
+        check(rc, "vissm_flow_kernel_precision")
+    return rc
+
+
 def _flow_params(w_eps, w_hid, b_hid, bn_g, bn_b, w_head, b_head, tf=None) -> FlowParams:
     """VissmFlowParams; tf = (theta [B, R], w_theta [R, H], b_theta [H]) is the theta branch's factorization
     (theta_term = theta w_theta + b_theta), which the two-sample AR kernels fold into their layer-0 product."""
@@ -282,8 +291,9 @@ class MAFlowFn(torch.autograd.Function):
         u = _rows(u, shape.L)
         pu = _pitch(u, shape.L)
         d = shape.desc(pu, _pitch(g_next, shape.Lout))
-        # the base noise needs no gradient: the bf16 kernels then skip the transposed convolution
-        need_du = ctx.needs_input_grad[2] or shape.precision == _lib.VISSM_PREC_FP32 or _FORCE_DU
+        # the base noise needs no gradient: the bf16 kernels then skip the transposed convolution (the exact-fp32
+        # kernels a shape beyond flow5 falls back to always write du)
+        need_du = ctx.needs_input_grad[2] or kernel_precision(shape) == _lib.VISSM_PREC_FP32 or _FORCE_DU
         du = _rows_empty(shape.B, shape.L, pu, dev) if need_du else None   # du rows at u's pitch
         dC = torch.empty_like(C)
         dth = torch.empty_like(theta_term)
