@@ -251,6 +251,16 @@ int vissm_elbo_fwd_theta_grad(const VissmElboDesc* d, const VissmElboData* data,
                               const float* g_extra, float* sde, float* obs, float* extra,
                               float* dtheta, void* stream);
 
+/* vissm_elbo_fwd and vissm_elbo_bwd in ONE pass over z, for upstream gradients known before the forward (the
+ * training step's loss -sum_b ELBO_b: g_sde = -scale, g_obs = -scale, g_extra = +scale per sample): sde, obs,
+ * extra (obs / extra may be NULL), dz and dtheta, every element's transition, obs row and ILDJ term evaluated once
+ * (the forward values are the backward's own transition records).  Replaces the two launches of the ELBO
+ * (AR.py:168-187, lotka_volterra_partial.py:234-297, SV_dense.py:203-232, fitz_nag_NVP.py:232-265 and their
+ * tf.gradients) for every model. */
+int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta,
+                        const float* g_sde, const float* g_obs, const float* g_extra, float* sde, float* obs,
+                        float* extra, float* dz, float* dtheta, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Global-norm clip + Adamax over one flat parameter buffer:
  * tf.global_norm / tf.clip_by_global_norm (AR.py:230-232) followed by

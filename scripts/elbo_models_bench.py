@@ -64,10 +64,15 @@ def main():
                                                     ptr(obs), ptr(ex), st), "fwd"),
             "bwd": lambda: check(lib.vissm_elbo_bwd(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(th), ptr(gs),
                                                     ptr(gs), ptr(gs), ptr(dz), ptr(dth), st), "bwd"),
+            # the training step's one pass (vissm_elbo_fwd_grad): values, dz and dtheta from one read of z
+            "one": lambda: check(lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(th),
+                                                         ptr(gs), ptr(gs), ptr(gs), ptr(sde), ptr(obs), ptr(ex),
+                                                         ptr(dz), ptr(dth), st), "one"),
         }
-        ts = {"fwd": [], "bwd": []}
+        kinds = [k for k in ("fwd", "bwd", "one") if k != "one" or hasattr(lib, "vissm_elbo_fwd_grad")]
+        ts = {k: [] for k in kinds}
         for _ in range(rounds):
-            for kind in ("fwd", "bwd"):
+            for kind in kinds:
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 calls[kind]()
                 torch.cuda.synchronize()
@@ -81,6 +86,10 @@ def main():
         f, b = min(ts["fwd"]), min(ts["bwd"])
         out[model] = {"fwd_ms": round(f, 4), "bwd_ms": round(b, 4), "fwd_frac": round(zb / (f * 1e-3) / 8e12, 3),
                       "bwd_frac": round(2 * zb / (b * 1e-3) / 8e12, 3), "check": [float(sde.double().sum()), float(dz.double().abs().sum())]}
+        if "one" in ts:
+            o = min(ts["one"])
+            out[model].update(one_ms=round(o, 4), one_frac=round(2 * zb / (o * 1e-3) / 8e12, 3),
+                              two_launch_ms=round(f + b, 4))
     print(json.dumps(out))
 
 

@@ -126,3 +126,67 @@ def test_model_elbo_kernels_match_oracle(model, M, n_win):
     assert torch.isfinite(zd.grad).all()
     assert rel(zd.grad, zr.grad) < 1e-4
     assert rel(thd.grad, thr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("M", [1, 3, 4, 5, 9, 50, 1001, 2000])
+@pytest.mark.parametrize("n_win", [1, 3])
+@pytest.mark.parametrize("model", ["ar", "lv", "sv", "fhn"])
+def test_one_pass_equals_forward_and_backward(model, M, n_win):
+    """vissm_elbo_fwd_grad (values, dz and dtheta from one read of z; the training step's ELBO for every model)
+    against the two launches it replaces: the values to fp32 summation order, dz bitwise (the same per-element
+    arithmetic), dtheta to summation order; and against the float64 oracle's values and autograd at the
+    two-launch bars (test above)."""
+    from viforssms_amd import _lib
+    from viforssms_amd.ops import ElboFeeds, elbo_terms, elbo_values_grad
+    B = 37
+    if model == "ar":
+        g = torch.Generator().manual_seed(M + n_win)
+        d = {"win": torch.randint(0, n_win, (B,), generator=g, dtype=torch.int32),
+             "z": torch.randn(B, M + 1, generator=g, dtype=torch.float64) * 3,
+             "theta": torch.stack([torch.randn(B, generator=g, dtype=torch.float64) * 0.3,
+                                   0.5 + 0.1 * torch.randn(B, generator=g, dtype=torch.float64),
+                                   0.2 * torch.randn(B, generator=g, dtype=torch.float64)], 1),
+             "obs": torch.randn(n_win, M, generator=g, dtype=torch.float64) * 3,
+             "bin": (torch.rand(n_win, M, generator=g, dtype=torch.float64) < 0.3).double(), "dt": 1.0}
+        for key in ("gs", "go"):
+            d[key] = torch.randn(B, generator=g, dtype=torch.float64)
+        obs_std = 1.3
+    else:
+        d = _case(model, B, M, n_win, seed=M * 7 + n_win + len(model))
+        obs_std = 1.0
+    f = lambda k: d[k].float().to(DEV).contiguous() if k in d else None
+    feeds = ElboFeeds(obs=f("obs"), obs_bin=f("bin"), mask=f("mask"), shift=f("shift"), dim_one=f("dim_one"),
+                      win=d["win"].to(DEV) if n_win > 1 else None, n_win=n_win)
+    mid = {"ar": _lib.MODEL_AR, "lv": _lib.MODEL_LV, "sv": _lib.MODEL_SV, "fhn": _lib.MODEL_FHN}[model]
+    gs, go = f("gs"), (f("go") if model != "sv" else torch.zeros(B, device=DEV))
+    ge = f("ge") if model == "lv" else None
+    zd = d["z"].float().to(DEV).requires_grad_(True)
+    thd = d["theta"].float().to(DEV).requires_grad_(True)
+    sde, obs, ex = elbo_terms(mid, M, d["dt"], obs_std, feeds, zd, thd)
+    dl = (sde * gs).sum() + (obs * go).sum() + ((ex * ge).sum() if ge is not None else 0.0)
+    dl.backward()
+    s1, o1, e1, dz1, dth1 = elbo_values_grad(mid, M, d["dt"], obs_std, feeds, zd.detach(), thd.detach(), gs, go, ge)
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double().cpu()
+        return float((a - b).norm() / (b.norm() + 1e-30))
+
+    assert rel(s1, sde) < 2e-6, rel(s1, sde)
+    if model != "sv":
+        assert rel(o1, obs) < 2e-6
+    if model == "lv":
+        assert float((e1 - ex).abs().max()) <= 2e-6 * float(ex.abs().max()) + 1e-6
+    assert torch.equal(dz1, zd.grad), float((dz1 - zd.grad).abs().max())
+    assert rel(dth1, thd.grad) < 1e-6
+    if model != "ar":
+        zr, thr = d["z"].clone().requires_grad_(True), d["theta"].clone().requires_grad_(True)
+        sde_r, obs_r, ex_r = _oracle(model, d, zr, thr)
+        loss = (sde_r * d["gs"]).sum()
+        if model != "sv":
+            loss = loss + (obs_r * d["go"]).sum()
+        if model == "lv":
+            loss = loss + (ex_r * d["ge"]).sum()
+        loss.backward()
+        assert rel(s1, sde_r) < 2e-5
+        assert rel(dz1, zr.grad) < 1e-4 and rel(dth1, thr.grad) < 1e-4

@@ -120,6 +120,7 @@ SIGNATURES = {
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_fwd_theta_grad": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData)] + [_c_void_p] * 10),
+    "vissm_elbo_fwd_grad": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData)] + [_c_void_p] * 11),
     "vissm_adamax_workspace_size": (_size_t, [_i64]),
     "vissm_adamax_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
                                  _f32, _c_void_p, _c_void_p, _size_t, _c_void_p]),

@@ -423,13 +423,20 @@ __global__ __launch_bounds__(256) void stream_fwd_kernel(Args a, const float* __
 // d/dz of gs sde + go obs + ge extra at every stored z entry, d/dtheta of gs sde.  Element e takes the
 // head gradient of transition e (e < M) and, for e >= 1, the tail gradient of transition e - 1 and the
 // obs / ILDJ terms observing x_e.
-template <int MODEL>
+// VALS (vissm_elbo_fwd_grad): the same pass also sums the forward values -- each element's head transition, the obs
+// row and the ILDJ term observing it are visited exactly once -- so the log-densities, dz and d theta come from one
+// read of z when the upstream gradients are known before the forward (the training step: -T/M and -1 per sample)
+struct Vals {
+  float *sde, *obs, *extra;
+};
+
+template <int MODEL, bool VALS = false>
 __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __restrict__ z,
                                                          const float* __restrict__ theta,
                                                          const float* __restrict__ g_sde,
                                                          const float* __restrict__ g_obs,
                                                          const float* __restrict__ g_ex, float* __restrict__ dz,
-                                                         float* __restrict__ dtheta) {
+                                                         float* __restrict__ dtheta, Vals vo = Vals{}) {
   using Dv = Dev<MODEL>;
   constexpr int ZD = Dv::ZD, P = Dv::P;
   const int lane = threadIdx.x & 63;
@@ -448,11 +455,18 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
   float acc[P];
 #pragma unroll
   for (int i = 0; i < P; ++i) acc[i] = 0.f;
+  float s_lp = 0.f, s_q = 0.f, s_b = 0.f, s_e = 0.f;  // VALS: the forward's per-sample sums
+  constexpr float isd = 1.f / Dv::kSd;
   // the gradient w.r.t. x_e of the terms observing x_e (obs row e - 1, ILDJ), e >= 1
   auto obs_g = [&](const St& s, float y0, float y1, float b0, float b1, float* g) {
     if constexpr (Dv::kObs) {
-      g[0] += cgo * b0 * (s.x[0] - y0);
-      g[1] += cgo * b1 * (s.x[1] - y1);
+      const float d0 = s.x[0] - y0, d1 = s.x[1] - y1;
+      g[0] += cgo * b0 * d0;
+      g[1] += cgo * b1 * d1;
+      if constexpr (VALS) {
+        s_q += b0 * (d0 * isd) * (d0 * isd) + b1 * (d1 * isd) * (d1 * isd);
+        s_b += b0 + b1;
+      }
     }
   };
   // the ILDJ term observing x_e (e >= 1), already w.r.t. the stored z
@@ -460,11 +474,13 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
     if constexpr (Dv::kExtra) {
       o0 += ge * s.dil[0];
       o1 += ge * s.dil[1];
+      if constexpr (VALS) s_e += s.il[0] + s.il[1];
     }
   };
   auto head = [&](const em::TG& r, float* g) {
     g[0] += gs * r.gh[0];
     g[1] += gs * r.gh[1];
+    if constexpr (VALS) s_lp += r.lp;
 #pragma unroll
     for (int i = 0; i < P; ++i) acc[i] += r.gth[i];
   };
@@ -553,20 +569,36 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
       else
         obs_g(sc, 0.f, 0.f, 0.f, 0.f, g);
     }
-    if (!dz) continue;
+    if (!VALS && !dz) continue;
     if constexpr (ZD == 2) {
       float o0 = g[0] * sc.j[0], o1 = g[1] * sc.j[1];
       if (t >= 1) ildj_dz(sc, o0, o1);
-      dzb[2 * t] = o0;
-      dzb[2 * t + 1] = o1;
+      if (dz) {
+        dzb[2 * t] = o0;
+        dzb[2 * t + 1] = o1;
+      }
     } else {
-      dzb[t] = g[1] * sc.j[1];
+      if (dz) dzb[t] = g[1] * sc.j[1];
     }
   }
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     const double s = wave_sum(static_cast<double>(acc[i]));
     if (lane == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(gs * s);
+  }
+  if constexpr (VALS) {
+    const double r_lp = wave_sum(static_cast<double>(s_lp));
+    const double r_q = wave_sum(static_cast<double>(s_q));
+    const double r_b = wave_sum(static_cast<double>(s_b));
+    const double r_e = wave_sum(static_cast<double>(s_e));
+    if (lane == 0) {
+      vo.sde[b] = static_cast<float>(r_lp);
+      if (vo.obs)
+        vo.obs[b] = Dv::kObs ? static_cast<float>(-0.5 * r_q + r_b * (-std::log(static_cast<double>(Dv::kSd)) -
+                                                                      0.5 * kLog2Pi))
+                             : 0.f;
+      if (vo.extra) vo.extra[b] = static_cast<float>(r_e);
+    }
   }
 }
 
@@ -685,11 +717,13 @@ __global__ __launch_bounds__(256) void ar_elbo_fwd_kernel(Args a, const float* _
 // d/dz of gs * sde + go * obs at times t in [0, M], and d/dtheta of gs * sde.  Element t takes the
 // head gradient of transition t (t < M) and the tail gradient of transition t - 1 plus its obs
 // term (t >= 1); each thread recomputes the transition before its chunk instead of exchanging it.
+// VALS (vissm_elbo_fwd_grad): also the forward's sums (sde, obs) in the same pass
+template <bool VALS = false>
 __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* __restrict__ z,
                                                           const float* __restrict__ theta,
                                                           const float* __restrict__ g_sde,
                                                           const float* __restrict__ g_obs, float* __restrict__ dz,
-                                                          float* __restrict__ dtheta) {
+                                                          float* __restrict__ dtheta, Vals vo = Vals{}) {
   const int lane = threadIdx.x & 63;
   const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kArW + (threadIdx.x >> 6));
   if (b >= a.B) return;  // wave-uniform
@@ -704,6 +738,7 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
   const float gs = g_sde ? g_sde[b] : 0.f, go = g_obs ? g_obs[b] : 0.f;
   const float cgh = gs * is * th1, cgt = -gs * is, cgo = -go * io;  // d/dx_t of the three terms per z / zo
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;  // sum_t of z_t, z_t x_t, z_t^2 - 1 over owned transitions
+  float so = 0.f, sb = 0.f;            // VALS: sum_t bin_t zo_t^2, sum_t bin_t
   // element t, given x_{t-1}, x_t, x_{t+1}: transition t (if t < M) and t - 1 (if t >= 1)
   auto elem = [&](int t, float xp, float xc, float xn, float y, float bn) -> float {
     float gx = 0.f;
@@ -716,7 +751,12 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
     }
     if (t >= 1) {
       const float zp = (xc - th1 * xp - th0) * is;
-      gx += cgt * zp + cgo * bn * (xc - y) * io;
+      const float zo = (xc - y) * io;
+      gx += cgt * zp + cgo * bn * zo;
+      if constexpr (VALS) {
+        so += bn * zo * zo;
+        sb += bn;
+      }
     }
     return gx;
   };
@@ -729,10 +769,15 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
       // all four elements are interior: t in [1, M)
       const float zt = (xs[j + 2] - th1 * xs[j + 1] - th0) * is;
       const float zp = (xs[j + 1] - th1 * xs[j] - th0) * is;
-      g[j] = cgh * zt + cgt * zp + cgo * bn[j] * (xs[j + 1] - y[j]) * io;
+      const float zo = (xs[j + 1] - y[j]) * io;
+      g[j] = cgh * zt + cgt * zp + cgo * bn[j] * zo;
       a0 += zt;
       a1 += zt * xs[j + 1];
       a2 += zt * zt - 1.f;
+      if constexpr (VALS) {
+        so += bn[j] * zo * zo;
+        sb += bn[j];
+      }
     }
     if (dz) *reinterpret_cast<f4u*>(dzb + t0) = g;
   };
@@ -776,6 +821,16 @@ __global__ __launch_bounds__(256) void ar_elbo_bwd_kernel(Args a, const float* _
     dtheta[b * 3 + 0] = static_cast<float>(gs * is * r0);
     dtheta[b * 3 + 1] = static_cast<float>(gs * is * r1);
     dtheta[b * 3 + 2] = static_cast<float>(gs * r2);
+  }
+  if constexpr (VALS) {
+    const double ro = wave_sum(static_cast<double>(so));
+    const double rb = wave_sum(static_cast<double>(sb));
+    if (lane == 0) {
+      // sum z^2 = sum (z^2 - 1) + M
+      vo.sde[b] = static_cast<float>(-0.5 * (r2 + M) + M * (-static_cast<double>(th2) - 0.5 * kLog2Pi));
+      if (vo.obs)
+        vo.obs[b] = static_cast<float>(-0.5 * ro + rb * (-std::log(static_cast<double>(a.obs_std)) - 0.5 * kLog2Pi));
+    }
   }
 }
 
@@ -861,7 +916,7 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   dim3 grid((d->B + kSW - 1) / kSW), blk(256);
   prof_begin(VISSM_PROF_ELBO_BWD, st);
   switch (d->model) {
-    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
+    case VISSM_MODEL_AR: hipLaunchKernelGGL(ar_elbo_bwd_kernel<false>, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde, g_obs, dz, dtheta); break;
     case VISSM_MODEL_LV: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_LV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_SV>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
     default: hipLaunchKernelGGL(stream_bwd_kernel<VISSM_MODEL_FHN>, grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta); break;
@@ -870,6 +925,33 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   // algorithmic bytes: z read, dz written, theta / dtheta and the upstream gradients
   prof_end(VISSM_PROF_ELBO_BWD, st,
            4.0 * d->B * ((dz ? 2.0 : 1.0) * zlen_of(d) + 2 * theta_len(d->model) + 3));
+  return VISSM_OK;
+}
+
+int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta,
+                        const float* g_sde, const float* g_obs, const float* g_extra, float* sde, float* obs,
+                        float* extra, float* dz, float* dtheta, void* stream) {
+  int rc = check(d, data);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(z && theta && sde && dz && dtheta, "elbo_fwd_grad: null pointer");
+  if (d->B == 0) return VISSM_OK;
+  Args a = make(d, data);
+  hipStream_t st = as_stream(stream);
+  dim3 grid((d->B + kSW - 1) / kSW), blk(256);
+  const Vals vo{sde, obs, extra};
+  prof_begin(VISSM_PROF_ELBO_BWD, st);
+  switch (d->model) {
+    case VISSM_MODEL_AR:
+      hipLaunchKernelGGL(ar_elbo_bwd_kernel<true>, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde,
+                         g_obs, dz, dtheta, vo);
+      break;
+    case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_SV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    default: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_FHN, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+  }
+  VISSM_CHECK_LAUNCH("elbo_fwd_grad");
+  // algorithmic bytes: z read once, dz written, theta / dtheta, the upstream gradients and the three sums
+  prof_end(VISSM_PROF_ELBO_BWD, st, 4.0 * d->B * (2.0 * zlen_of(d) + 2 * theta_len(d->model) + 6));
   return VISSM_OK;
 }
 

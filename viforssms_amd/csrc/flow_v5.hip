@@ -49,6 +49,13 @@
 #endif
 
 #include <cstdlib>
+// VISSM_ABL_STORES (diagnostic builds only, results wrong): bit 0 drops the fused variant's x stores, bit 1 the du
+// stores, bit 2 the dC slab stores -- per-buffer attribution of the backward's PMC WRITE_SIZE
+#ifndef VISSM_ABL_STORES
+#define VISSM_ABL_STORES 0
+#endif
+// du of a full 16-position tile as four 16-byte stores per sample (lanes q = 4i gather q .. q + 3 by DPP row shifts)
+// where the row pitch and the tile start are 4-float aligned (padded flow rows: every middle flow); dword stores else
 
 namespace vissm {
 namespace VISSM_FLOW5_NS {
@@ -1307,6 +1314,14 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 constexpr int NW2 = 8;
 constexpr int NT2 = 64 * NW2;
+#ifndef VISSM_DU_X4
+#define VISSM_DU_X4 1
+#endif
+template <int N>
+__device__ __forceinline__ float row_shl_n(float v) {  // lane c <- lane c + N within its row of 16
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0x100 + N, 0xf, 0xf, false));
+}
 constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 // Design decisions (A/B, AR-cfg launches):
 //  * compiler fences between the unit's phases in the fused (FZ) variant only (without them: middle flows 23.3 ->
@@ -1620,7 +1635,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           if (g == 0) {
             if constexpr (NPR == 1) gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the du section reads
             if (pv && (cb == 0 || two)) {
-              fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
+              if constexpr (!(VISSM_ABL_STORES & 1)) fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
               if constexpr (ZLS) zls[w][bl2][c] += lsg;
             }
           }
@@ -1821,7 +1836,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         fence2<FZ>();
         const int cbq = lane >> 5, q = lane & 31;
         const int lim = nP + a.k;
-        if (q < lim && (cbq == 0 || two)) {
+        const bool act = q < lim && (cbq == 0 || two);
+        const int blq = cbq ? blv[1] : blv[0];
+        float v = 0.f;
+        if (act) {
           const int qc = q < QW2 ? q : QW2 - 1;
           float t[KP2];
 #pragma unroll
@@ -1830,18 +1848,32 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int w2 = 1; w2 < KP2; w2 *= 2)
 #pragma unroll
             for (int j = 0; j + w2 < KP2; j += 2 * w2) t[j] += t[j + w2];
-          float v = t[0];
+          v = t[0];
           const int oq2 = q - a.k;
           if (oq2 >= 0 && oq2 < nP) v += NPR == 2 ? gwin[w][cbq][oq2] : gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
-          const int blq = cbq ? blv[1] : blv[0];
           if (q < a.k) v += carry[w][blq][q];
-          if (q < nP) du[static_cast<size_t>(b_lo + blq) * a.pL + t0 + q] = v;
-          else carry[w][blq][q - nP] = v;
+        }
+        float* const dur = du + static_cast<size_t>(b_lo + blq) * a.pL + t0;
+        if (!FZ && VISSM_DU_X4 && nP == P && ((a.pL | t0) & 3) == 0) {  // wave-uniform
+          const float v1 = row_shl_n<1>(v), v2 = row_shl_n<2>(v), v3 = row_shl_n<3>(v);
+          if (act) {
+            if (q < P) {
+              if ((q & 3) == 0 && !(VISSM_ABL_STORES & 2)) *reinterpret_cast<f4*>(dur + q) = f4{v, v1, v2, v3};
+            } else {
+              carry[w][blq][q - P] = v;
+            }
+          }
+        } else if (act) {
+          if (q < nP) {
+            if constexpr (!(VISSM_ABL_STORES & 2)) dur[q] = v;
+          } else {
+            carry[w][blq][q - nP] = v;
+          }
         }
       }
     }
     // tile done: its dC over the group (both samples of every pair)
-    if (c < nP) {
+    if (c < nP && !(VISSM_ABL_STORES & 4)) {
       const size_t row = (static_cast<size_t>(grp) * a.Lh + m0 + c) * a.H;
       if (a.dc16) {
         __bf16* dcs = reinterpret_cast<__bf16*>(dC_slab) + row;

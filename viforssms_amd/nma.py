@@ -25,7 +25,8 @@ import torch
 
 from . import _lib
 from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
-                  ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad)
+                  ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad,
+                  elbo_values_grad)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, linear_bf16, linear_x3, tn_split_k
@@ -471,6 +472,62 @@ class Engine:
     # ---- forward ----
     def forward(self, batch: Batch, eps: torch.Tensor, base_lp: Optional[torch.Tensor], x0_theta: torch.Tensor):
         md = self.mdef
+        z, lq, theta, logq_theta = self._flows_forward(batch, eps, base_lp, x0_theta)
+        sde, obs, extra = elbo_terms(md.model_id, md.M, md.dt, md.obs_std, batch.feeds, z, theta)
+        if md.family == "lv":
+            lq = lq + extra
+        prior = self.prior_logprob(theta)
+        scale = md.scale_num / md.M
+        if md.family == "sv":
+            elbo = scale * (sde - lq) + prior - logq_theta
+        else:
+            elbo = scale * (sde - lq + obs) + prior - logq_theta
+        return {"elbo": elbo, "sde": sde, "obs": obs, "logq": lq, "theta": theta, "logq_theta": logq_theta,
+                "prior": prior, "z": z}
+
+    def onepass_ok(self) -> bool:
+        """The training step can take the ELBO's values and gradients from one pass over z (vissm_elbo_fwd_grad);
+        VISSM_ELBO_ONEPASS=0 keeps the forward + backward launches (A/B)."""
+        return os.environ.get("VISSM_ELBO_ONEPASS", "1") != "0"
+
+    def forward_onepass(self, batch: Batch, eps: torch.Tensor, base_lp: Optional[torch.Tensor],
+                        x0_theta: torch.Tensor):
+        """The training step's ELBO with the log-density terms in one pass over the path (vissm_elbo_fwd_grad): the
+        loss is -sum_b ELBO_b, so the upstream gradients of (sde, obs, extra) are the constants (-scale, -scale or 0
+        for SV, +scale for LV's ILDJ term, which enters log q) before the forward runs.  Returns (out, (roots,
+        grads)) as forward_fused: autograd from the scalar root for the terms outside the log-densities (flows' log
+        sigma, prior, q(theta)), dz and dtheta fed in at z and theta."""
+        md = self.mdef
+        z, lq, theta, logq_theta = self._flows_forward(batch, eps, base_lp, x0_theta)
+        B = z.shape[0]
+        scale = md.scale_num / md.M
+        dev = z.device
+        gs = torch.full((B,), -scale, dtype=torch.float32, device=dev)
+        go = gs if md.family != "sv" else torch.zeros_like(gs)
+        ge = torch.full((B,), scale, dtype=torch.float32, device=dev) if md.family == "lv" else None
+        th = theta.detach().contiguous()
+        sde, obs, extra, dz, dth = elbo_values_grad(md.model_id, md.M, md.dt, md.obs_std, batch.feeds, z.detach(),
+                                                    th, gs, go, ge)
+        prior = self.prior_logprob(theta)
+        rest = scale * (-lq) + prior - logq_theta            # ELBO terms outside the log-densities (autograd)
+        roots = [(-rest).sum(), z, theta]
+        grads = [None, dz.view_as(z), dth]
+        keep = [i for i, r in enumerate(roots) if r.requires_grad]
+        roots, grads = [roots[i] for i in keep], [grads[i] for i in keep]
+        lq_out = lq.detach() + (extra if md.family == "lv" else 0.0)
+        if md.family == "sv":
+            elbo = scale * (sde - lq_out) + prior.detach() - logq_theta.detach()
+        else:
+            elbo = scale * (sde - lq_out + obs) + prior.detach() - logq_theta.detach()
+        out = {"elbo": elbo, "sde": sde, "obs": obs, "logq": lq_out, "theta": th, "logq_theta": logq_theta.detach(),
+               "prior": prior.detach(), "z": z.detach()}
+        return out, (roots, grads)
+
+    def _flows_forward(self, batch: Batch, eps: torch.Tensor, base_lp: Optional[torch.Tensor],
+                       x0_theta: torch.Tensor):
+        """q(theta) and the flow stack: the path z, log q of the flows (base log-prob minus the log sigma sums),
+        theta and log q(theta), all in the autograd graph."""
+        md = self.mdef
         if base_lp is None:
             base_lp = base_logprob(eps, md.n_logsig)
         theta, logq_theta = self.theta_dist.sample_and_log_prob(x0_theta)
@@ -491,18 +548,7 @@ class Engine:
             u, ls = fl.flow(shape, batch.win, u, C, tt, self.theta_fold(fl, theta), grad_sum=self.grad_sum)
             lq = lq - ls
             L -= md.k
-        z = u
-        sde, obs, extra = elbo_terms(md.model_id, md.M, md.dt, md.obs_std, batch.feeds, z, theta)
-        if md.family == "lv":
-            lq = lq + extra
-        prior = self.prior_logprob(theta)
-        scale = md.scale_num / md.M
-        if md.family == "sv":
-            elbo = scale * (sde - lq) + prior - logq_theta
-        else:
-            elbo = scale * (sde - lq + obs) + prior - logq_theta
-        return {"elbo": elbo, "sde": sde, "obs": obs, "logq": lq, "theta": theta, "logq_theta": logq_theta,
-                "prior": prior, "z": z}
+        return u, lq, theta, logq_theta
 
     # ---- the last AR(1) flow fused with its ELBO terms (training step) ----
     def _last_shape(self, batch: Batch, B: int) -> FlowShape:

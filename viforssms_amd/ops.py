@@ -463,6 +463,28 @@ def elbo_values_and_theta_grad(model: int, M: int, dt: float, obs_std: float, fe
     return sde, obs, dth
 
 
+def elbo_values_grad(model: int, M: int, dt: float, obs_std: float, feeds: ElboFeeds, z, theta,
+                     g_sde: torch.Tensor, g_obs: Optional[torch.Tensor], g_extra: Optional[torch.Tensor]):
+    """(sde, obs, extra) per sample, dz and dtheta of g_sde . sde + g_obs . obs + g_extra . extra in ONE pass over z
+    (vissm_elbo_fwd_grad): the training step knows these upstream gradients before the forward.  No autograd: the
+    caller feeds dz / dtheta into a multi-root backward (Engine.forward_onepass)."""
+    lib = _lib.load()
+    _require_gpu(z, theta, g_sde, feeds.obs, feeds.obs_bin, feeds.mask, feeds.shift, feeds.dim_one, feeds.win)
+    B = z.shape[0]
+    d = ElboDesc(model, B, M, feeds.n_win, float(dt), float(obs_std))
+    data = feeds.cdata()
+    sde = torch.empty(B, dtype=torch.float32, device=z.device)
+    obs = torch.empty_like(sde)
+    extra = torch.empty_like(sde)
+    z = z.contiguous()
+    dz = torch.empty_like(z)
+    dth = torch.empty_like(theta)
+    check(lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(theta), ptr(g_sde), ptr(g_obs),
+                                  ptr(g_extra), ptr(sde), ptr(obs), ptr(extra), ptr(dz), ptr(dth),
+                                  _lib.stream_handle(z.device)), "vissm_elbo_fwd_grad")
+    return sde, obs, extra, dz, dth
+
+
 # ---------------------------------------------------------------------------------------
 # optimiser
 # ---------------------------------------------------------------------------------------

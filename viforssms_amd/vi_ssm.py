@@ -199,6 +199,18 @@ class VISSMBase:
             self._arm_overlap()
             torch.autograd.backward(roots, grads)
             del roots, grads
+        elif self.engine.onepass_ok():
+            # the log-densities' values, dz and dtheta from one pass over the path (vissm_elbo_fwd_grad: the loss's
+            # upstream gradients are constants), the rest of the gradient through autograd (multi-root backward)
+            e, bl, x0 = self._draws(batch, step, eps, x0_theta, row0_dev)
+            self.engine.grad_sum = self.dist if shared else None
+            try:
+                out, (roots, grads) = self.engine.forward_onepass(batch, e, bl, x0)
+            finally:
+                self.engine.grad_sum = None
+            self._arm_overlap(shared)
+            torch.autograd.backward(roots, grads)
+            del roots, grads
         else:
             self.engine.grad_sum = self.dist if shared else None
             try:
