@@ -3,7 +3,7 @@
 # ROUNDS rounds):
 # ms per step, backward per launch (average and per variant), roofline fraction.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
+ROOT=$(pwd); OUT=${OUT:-$ROOT/gpurun_out}; mkdir -p "$OUT"
 for r in $(seq 1 ${ROUNDS:-2}); do for L in ${@:-abl/*.so}; do
   n=$(basename $L .so)
   VISSM_LIB=$ROOT/$L timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 2 --cpu-baseline off \

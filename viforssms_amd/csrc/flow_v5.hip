@@ -1314,9 +1314,19 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 constexpr int NW2 = 8;
 constexpr int NT2 = 64 * NW2;
+// bwd2: the pair's head backward in one pass, one sample per lane-group pair (VISSM_BWD2_HEADSHARE=0: once per sample)
+#ifndef VISSM_BWD2_HEADSHARE
+#define VISSM_BWD2_HEADSHARE 1
+#endif
 #ifndef VISSM_DU_X4
 #define VISSM_DU_X4 1
 #endif
+// lanes 32..63 of v into lanes 0..31 (v_permlane32_swap); lanes 32..63 of the result keep v's
+__device__ __forceinline__ float swap_hi_lo(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, static_cast<unsigned>(r[1]));
+}
 template <int N>
 __device__ __forceinline__ float row_shl_n(float v) {  // lane c <- lane c + N within its row of 16
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
@@ -1609,10 +1619,81 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           put_image<NP>(im1 + cb * P * HP, nullptr, X[cb], g, c);  // I_1 (head input) with its ones row
         }
       }
-      // ---- head backward, per sample
+      // ---- head backward
       const bool pv = c < nP;
-      float sig[2], gmu[2], gr[2];
+      float gmu[2], gr[2];
       float lsv[2] = {0.f, 0.f};  // fused variant without the LDS column sums: the output columns' log sigma
+#if VISSM_BWD2_HEADSHARE
+      // Both samples' head backward in one pass: lane groups 0, 1 evaluate sample A's columns and 2, 3 sample B's
+      // (the head MFMA left every column's (mu, r) in all four groups), so the softplus / sigmoid / upstream-gradient
+      // work runs once per pair instead of once per sample; v_permlane32_swap then brings B's (g_mu, g_r) from groups
+      // 2, 3 to 0, 1, where the dZ product's B operand (group 0) and the I_1 image rows (group 1) take them.
+      {
+        const int hs = g >> 1;                      // the sample of this lane's head work
+        const bool hv = hs == 0 || two;             // not the ghost
+        const float mu_h = hs ? mu[1] : mu[0], rr_h = hs ? rr[1] : rr[0];
+        const float sig_h = softplus_fast(rr_h) + 1e-10f;
+        const float uk = uwin[w][hs][c + a.k];
+        float gmu_h, lsv_h = 0.f;
+        if constexpr (FZ) {
+          const float x = uk * sig_h + mu_h;
+          float xp = row_prev(x);
+          const float xn = row_next(x);
+          if (c == 0) xp = hs ? fz_zc[1] : fz_zc[0];
+          const int bl2 = hs ? blv[1] : blv[0];
+          const float th0 = hs ? lane_f(lt0, blv[1]) : lane_f(lt0, blv[0]);
+          const float th1 = hs ? lane_f(lt1, blv[1]) : lane_f(lt1, blv[0]);
+          const float is = hs ? lane_f(lis, blv[1]) : lane_f(lis, blv[0]);
+          const int t = m0 + c;
+          const float fh = (pv && t < fz.M) ? 1.f : 0.f;
+          const float ft = (pv && t >= 1) ? 1.f : 0.f;
+          const float bp = fz_bp * ft;
+          const float zt = fh * (xn - th1 * x - th0) * is;
+          const float zp = ft * (x - th1 * xp - th0) * is;
+          const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
+          gmu_h = hv ? -fz.scale * de : 0.f;
+          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig_h) * kLn2 : 0.f;
+          if ((g & 1) == 0) {  // lane groups 0 (A) and 2 (B)
+            if constexpr (NPR == 1) gwin[w][hs][c] = gmu_h;  // the upstream-gradient window the du section reads
+            if (pv && hv) {
+              if constexpr (!(VISSM_ABL_STORES & 1)) fz.x[static_cast<size_t>(b_lo + bl2) * (fz.M + 1) + t] = x;
+              if constexpr (ZLS) zls[w][bl2][c] += lsg;
+            }
+          }
+          if constexpr (!ZLS) lsv_h = (pv && hv) ? lsg : 0.f;
+          if ((lane & 31) == PO - 1 && (nP == PO || discard) && hv) zcar[w][bl2] = x;
+        } else {
+          gmu_h = pv ? gwin[w][hs][c] : 0.f;
+        }
+        const float dl = FZ ? -fz.scale : (hs ? lane_f(ldl, blv[1]) : lane_f(ldl, blv[0]));
+        float dsig = gmu_h * uk;
+        if (pv && hv && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig_h);
+        const float gr_h = dsig * sigmoid_fast(rr_h);
+        if ((g & 1) == 0) {
+          if constexpr (NPR == 2) {
+            if constexpr (DU) gwin[w][hs][c] = gmu_h * sig_h;  // (after the reads of g_mu above: LDS order)
+          } else {
+            gsc[w][hs][c] = sig_h;
+          }
+        }
+        gmu[0] = gmu_h;
+        gr[0] = gr_h;
+        gmu[1] = swap_hi_lo(gmu_h);
+        gr[1] = swap_hi_lo(gr_h);
+        if constexpr (FZ && !ZLS) {
+          lsv[0] = lsv_h;
+          lsv[1] = swap_hi_lo(lsv_h);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        if (g == 1) {
+          const int off = timg_off(c, 4 * 3 + 1);
+          *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
+        }
+      }
+#else
+      float sig[2];
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         sig[cb] = softplus_fast(rr[cb]) + 1e-10f;
@@ -1666,6 +1747,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
         }
       }
+#endif
       fence2<FZ>();
       // dW_head[h][o] += sum over both samples' positions of I_1[h][p] G[o][p] (K = 32): block 3 of the same
       // fragments is the B operand (its columns 5, 6 are the G rows)
