@@ -21,60 +21,7 @@ from oracle import nma_oracle as O  # noqa: E402
 from oracle import bridge  # noqa: E402
 from tests.parity_util import build_model, oracle_inputs  # noqa: E402
 
-MODE = {}
-
-
-def rb(x):
-    return x.float().bfloat16().double()
-
-
-def R(x, key):
-    return rb(x) if MODE.get(key, False) else x
-
-
-class BMM(torch.autograd.Function):
-    """y = x @ W with the kernel's operand roundings (x activations [..., K], W weights [K, N])."""
-
-    @staticmethod
-    def forward(ctx, x, W):
-        ctx.save_for_backward(x, W)
-        return R(x, "fwd_x") @ R(W, "fwd_w")
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, W = ctx.saved_tensors
-        g = R(gy, "bwd_g")
-        gx = g @ R(W, "bwd_w").t()
-        xr = R(R(x, "fwd_x"), "wg_x")     # the kernels' weight-gradient products read the bf16 images
-        gW = (xr.reshape(-1, x.shape[-1]).t() @ g.reshape(-1, g.shape[-1]))
-        return gx, gW
-
-
-class GradRound(torch.autograd.Function):
-    """identity; the backward rounds the gradient (dC and d theta_term sum the bf16 dA0 image)"""
-
-    @staticmethod
-    def forward(ctx, x):
-        return x.view_as(x)
-
-    @staticmethod
-    def backward(ctx, g):
-        return R(g, "bwd_g")
-
-
-def iaf_flow_emul(u, CF, theta, P, cfg):
-    w = P["conv_w"][:, 0, :]                       # [k, H]
-    k = w.shape[0]
-    x = u[:, :-1]
-    n_out = x.shape[1] - k + 1
-    U = x.unfold(1, k, 1)                           # [p, n_out, k]
-    a = BMM.apply(U, w) + GradRound.apply(CF + O.theta_term(theta, P)[:, None, :])
-    h = O.elu(a)
-    for l in range(cfg.n_hidden):
-        h = O.elu(BMM.apply(h, P[f"hid_w{l}"]) + P[f"hid_b{l}"])
-    head = BMM.apply(h, P["head_w"]) + P["head_b"]
-    mu, sig = head[..., 0], O.softplus(head[..., 1]) + 1e-10
-    return u[:, cfg.k:] * sig + mu, torch.log(sig[:, -cfg.n_logsig:])
+from oracle.precision_model import MODE, iaf_flow_emul  # noqa: E402  (the rounding model, shared with the tests)
 
 
 MODES = {

@@ -222,11 +222,15 @@ def oracle_reference(model, batch, eps: torch.Tensor, x0: torch.Tensor):
 def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n_layers: int, fw: int,
                     device: str = "cuda:0", T: Optional[int] = None, starts=None, precision: int = 0,
                     seed: int = 3, impute: Optional[int] = None, condition: bool = False,
-                    fp32_yardstick: bool = False, step_path: bool = False, chunk_tiles: int = 0) -> Dict:
+                    fp32_yardstick: bool = False, step_path: bool = False, chunk_tiles: int = 0,
+                    emulate: bool = False) -> Dict:
     """step_path: the product side runs the training step's gradient (VI_SSM.elbo_step without the
     Adamax apply: for AR at bf16 / bf16x3 the last flow fused with the ELBO terms) instead of
     forward + autograd backward.  chunk_tiles > 0 forces the flow kernels' tiles per t-chunk
-    (VissmFlowDesc.chunk_tiles): the launch geometry of a larger batch at this batch."""
+    (VissmFlowDesc.chunk_tiles): the launch geometry of a larger batch at this batch.
+    emulate: also evaluate the oracle under the precision's rounding model (oracle/precision_model.py: bf16 / bf16x2f
+    / bf16x2) and return its errors against the exact oracle ("emul": the tolerance source of a reduced-precision
+    case, emulated_tol)."""
     torch.cuda.set_device(torch.device(device))
     model = build_model(family, B, M, k, n_flows, H, n_layers, fw, device, T=T, precision=precision, seed=seed,
                         impute=impute, condition=condition)
@@ -271,6 +275,21 @@ def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n
     for n in st.names():
         r, q = ref_g[n], grads_gpu[n]
         per[n] = float(np.linalg.norm(q - r) / (np.linalg.norm(r) + 1e-6 * gnorm + 1e-30))
+    emul = None
+    if emulate:
+        from oracle.precision_model import PRECISION_MODE, emulate as _emulate
+        mode = PRECISION_MODE[precision]
+        errs = []
+        for seed in range(EMUL_REALISATIONS):   # the plain emulation and jittered realisations (envelope)
+            with _emulate(mode, jitter=2.0 ** -22 if seed else 0.0, seed=seed):
+                e_em, g_em = oracle_reference(model, batch, eps, x0)
+            gem = np.concatenate([g_em[n].ravel() for n in st.names()])
+            errs.append((float(np.max(np.abs(e_em - elbo_ref) / np.maximum(np.abs(elbo_ref), 1e-6))),
+                         float(np.linalg.norm(gem - gref) / (gnorm + 1e-30)),
+                         max(float(np.linalg.norm(g_em[n] - ref_g[n]) / (np.linalg.norm(ref_g[n]) + 1e-6 * gnorm
+                                                                           + 1e-30)) for n in st.names())))
+        emul = {"mode": mode, "elbo_rel_err": max(e[0] for e in errs), "grad_rel_err": max(e[1] for e in errs),
+                "grad_max_param_err": max(e[2] for e in errs)}
     return {
         "fused": bool(step_path and model.engine.fused_ok(batch, B)),
         "elbo_rel_err": elbo_err,
@@ -281,4 +300,22 @@ def run_parity_case(family: str, B: int, M: int, k: int, n_flows: int, H: int, n
         "per_param": per,
         "finite": bool(np.isfinite(elbo_gpu).all() and np.isfinite(ggpu).all()),
         "elbo_rel_err_fp32_oracle": fp32_err,
+        "emul": emul,
     }
+
+
+# realisations of the rounding model per emulated case (plain + jittered): the envelope a GPU realisation is held to
+EMUL_REALISATIONS = 3
+# a reduced-precision case passes when each error is within SAFETY x the rounding model's envelope + the fp32 bar
+EMUL_SAFETY = 3.0
+FP32_BAR = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
+
+
+def emulated_tol(res: Dict, safety: float = EMUL_SAFETY) -> Dict:
+    """Tolerances of a reduced-precision case from its precision's rounding model (run_parity_case(emulate=True)):
+    safety x the emulated error + the fp32 bar -- derived from the mode's arithmetic, not from a measurement of the
+    kernels."""
+    em = res["emul"]
+    return dict(elbo_tol=safety * em["elbo_rel_err"] + FP32_BAR["elbo_tol"],
+                grad_tol=safety * em["grad_rel_err"] + FP32_BAR["grad_tol"],
+                param_tol=safety * em["grad_max_param_err"] + FP32_BAR["param_tol"])

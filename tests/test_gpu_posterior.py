@@ -55,26 +55,33 @@ def _post_stats(theta):
 #  * fp32 at the paper shape (the reference's own configuration): posterior mean / sd within 10x the
 #    float32 oracle's own drift from the float64 trajectory + 2e-5 absolute, per-sample ELBO within 1e-4
 #    (or 10x the float32 oracle's error where the step's ELBO is an ill-conditioned cancellation);
-#  * bf16x2f at the AR-cfg length (BASELINE configs[1]'s window, where that precision holds the ELBO to
-#    1e-4: tests/test_gpu_config_parity.py): the first step's ELBO (same parameters on both sides) within
-#    1e-4; after it the parameters differ by the bf16 gradients' Adamax steps (its backward products are
-#    bf16, and Adamax's normalised steps pass a gradient's rounding straight into the parameters: measured
-#    ELBO 1.5e-3 and posterior mean 6e-4 apart after 10 steps), so ELBO within 5e-3 and posterior mean / sd
-#    within 5e-3 absolute; that the bf16 path trains to the same posterior is test (b) at bf16
+#  * the reduced-precision modes at the AR-cfg length (BASELINE configs[1]'s window): their flow products round
+#    operands by design and Adamax's normalised steps pass those roundings into the parameters, so their bar comes
+#    from the modes' rounding model, not from a measurement of the kernels: scripts/precision_drift_emul.py runs the
+#    same K steps in float64 under each mode's rounding (oracle/precision_model.py; plain + jittered realisations)
+#    against the exact trajectory (tests/golden/precision_drift.json); after step s the GPU must stay within
+#    EMUL_SAFETY x the envelope's running maximum up to s + the fp32 case's floor (2e-5 on the posterior, 1e-4 on the
+#    ELBO).  At step 0 the parameters are identical, so the ELBO bar is the forward precision's alone.
 TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO tolerance at step 0, after)
     "fp32": (50, 50, 50, 5000, 10.0, 2e-5, 1e-4, 1e-4),
-    "bf16x2f": (20, 5000, 8, 5000, 0.0, 5e-3, 1e-4, 5e-3),
-    # bf16x2 (split weights in the backward chain too: gradient within 1e-3).  Measured (profiles/r04/
-    # pytest_posterior_bf16x2.log): the posterior stays within the fp32 case's bar (10x the float32 oracle's drift +
-    # 2e-5) for 16 steps (<= 1.6e-5), then drifts to 8.9e-5 by step 20 -- Adamax's normalised steps pass the
-    # gradient's ~1e-4 relative error (bf16 gradient operands) into the parameters; the ELBO 2.3e-5 at the first step,
-    # <= 9.3e-4 after.  Held to 10x the float32 drift + 1.5e-4 and ELBO 1e-4 / 2e-3.  (bf16: 2.9e-3 and 1.4e-2.)
-    "bf16x2": (20, 5000, 8, 5000, 10.0, 1.5e-4, 1e-4, 2e-3),
-    # bf16, the headline precision: measured over 20 steps (profiles/r04/pytest_gpu_full_first.log) posterior mean / sd
-    # 2.9e-3 / 2.5e-3 from the float64 trajectory (growing ~linearly: Adamax passes the bf16 gradients' rounding into
-    # every step), ELBO 1.1e-3 at the first step, 1.4e-2 worst after; held to 5e-3, 5e-3 and 2e-2
-    "bf16": (20, 5000, 8, 5000, 0.0, 5e-3, 5e-3, 2e-2),
+    "bf16x2f": (20, 5000, 8, 5000, 0.0, 2e-5, 1e-4, 1e-4),
+    "bf16x2": (20, 5000, 8, 5000, 0.0, 2e-5, 1e-4, 1e-4),
+    "bf16": (20, 5000, 8, 5000, 0.0, 2e-5, 1e-4, 1e-4),
 }
+EMUL_SAFETY = 3.0
+
+
+def _envelope(prec, K):
+    """Running maxima of the rounding model's drift per step (dmean, dsd, elbo) for a reduced-precision mode."""
+    import json
+    path = os.path.join(ROOT, "tests", "golden", "precision_drift.json")
+    rows = json.load(open(path))["modes"][prec]
+    assert len(rows) >= K, "tests/golden/precision_drift.json has fewer steps than the trajectory"
+    env, cur = [], {"dmean": 0.0, "dsd": 0.0, "elbo": 0.0}
+    for r in rows[:K]:
+        cur = {key: max(cur[key], r[key]) for key in cur}
+        env.append(dict(cur))
+    return env
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16x2f", "bf16x2", "bf16"])
@@ -104,6 +111,7 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
             th, _ = model.engine.theta_dist.sample_and_log_prob(xe.float().to(DEV))
         return _post_stats(th)
 
+    env = _envelope(prec, K) if prec != "fp32" else None
     m0, _ = post_oracle(P[64], torch.float64)
     np.random.seed(5)
     worst = {"dmean": 0.0, "dsd": 0.0, "elbo": 0.0}
@@ -139,17 +147,19 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
         # (the whole trajectory runs and prints before the assertions, so a failure shows every step's numbers)
         if not (np.isfinite(eg).all() and np.isfinite(mg).all()):
             bad.append((step, "non-finite"))
-        if dgm > mult * d32m + floor:
-            bad.append((step, "posterior mean", dgm, d32m))
-        if dgs > mult * d32s + floor:
-            bad.append((step, "posterior sd", dgs, d32s))
-        if erel > max(elbo_tol0 if step == 0 else elbo_tol, 10 * erel32):
-            bad.append((step, "ELBO", erel, erel32))
+        em = env[step] if env is not None else {"dmean": 0.0, "dsd": 0.0, "elbo": 0.0}
+        if dgm > mult * d32m + EMUL_SAFETY * em["dmean"] + floor:
+            bad.append((step, "posterior mean", dgm, d32m, em["dmean"]))
+        if dgs > mult * d32s + EMUL_SAFETY * em["dsd"] + floor:
+            bad.append((step, "posterior sd", dgs, d32s, em["dsd"]))
+        if erel > max((elbo_tol0 if step == 0 else elbo_tol) + EMUL_SAFETY * em["elbo"], 10 * erel32):
+            bad.append((step, "ELBO", erel, erel32, em["elbo"]))
         worst = {"dmean": max(worst["dmean"], dgm), "dsd": max(worst["dsd"], dgs), "elbo": max(worst["elbo"], erel)}
     print("worst over the trajectory:", worst)
     assert not bad, bad
     # the trajectory moved the posterior by more than the tolerance (the comparison is not vacuous)
-    assert np.abs(ma - m0).max() > 5 * floor
+    final_bar = floor + (EMUL_SAFETY * env[-1]["dmean"] if env is not None else 0.0)
+    assert np.abs(ma - m0).max() > 5 * floor and np.abs(ma - m0).max() > final_bar, (np.abs(ma - m0).max(), final_bar)
 
 
 RECOVERY_STEPS = int(os.environ.get("VISSM_RECOVERY_STEPS", "10000"))

@@ -313,12 +313,13 @@ def test_flow_kernel_precision_query():
 
 
 @pytest.mark.parametrize("family,k", [("lv", 4), ("ar", 50)])
-@pytest.mark.parametrize("prec", ["bf16x2", "bf16x2f"])
-def test_engine_refuses_bf16x2_beyond_split_kernels(family, k, prec):
+def test_engine_refuses_bf16x2_beyond_split_kernels(family, k):
     """bf16x2 on LV / SV / FHN or AR with k > 32 used to run an fp32 forward under the bf16x2 label and
-    then stop in the first backward (du = NULL on the fp32 kernels); the engine now refuses it up front."""
+    then stop in the first backward (du = NULL on the fp32 kernels); the engine now refuses it up front.  bf16x2f
+    (forward split weights or exact fp32, backward bf16) stays valid there."""
     from tests.parity_util import build_model
     from viforssms_amd import _lib
+    nl = 5 if family == "lv" else 3
     with pytest.raises(ValueError, match="bf16x2"):
-        build_model(family, 4, 24, k, 2, 16, 5 if family == "lv" else 3, 3, "cpu",
-                    precision=_lib.TRAIN_PRECISIONS[prec])
+        build_model(family, 4, 24, k, 2, 16, nl, 3, "cpu", precision=_lib.TRAIN_PRECISIONS["bf16x2"])
+    build_model(family, 4, 24, k, 2, 16, nl, 3, "cpu", precision=_lib.TRAIN_PRECISIONS["bf16x2f"])

@@ -30,7 +30,10 @@ struct Args {
 // ---------------------------------------------------------------------------
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-constexpr int kV = 4;   // times per chunk
+#ifndef VISSM_ELBO_KV
+#define VISSM_ELBO_KV 4
+#endif
+constexpr int kV = VISSM_ELBO_KV;   // times per chunk (A/B builds: VISSM_ELBO_KV=8)
 constexpr int kSU = 2;  // chunks per lane in flight
 constexpr int kSW = 4;  // trajectories (waves) per 256-thread block
 

@@ -399,10 +399,13 @@ class Engine:
         self._check_precision()
 
     def _check_precision(self):
-        """bf16x2 / bf16x2f are throughput modes of the split-weight matrix-core kernels (one hidden layer, k <= 32:
-        the AR configurations).  Elsewhere the flow calls would fall back to the exact-fp32 kernels and the mode's
-        name would misstate what ran, so the engine refuses it up front (vissm_flow_kernel_precision)."""
-        if self.precision not in (_lib.VISSM_PREC_BF16X2, _lib.VISSM_PREC_BF16X2F):
+        """bf16x2 is the split-weight mode of the one-hidden-layer matrix-core kernels (k <= 32: the AR
+        configurations), forward and backward.  Elsewhere every flow call would fall back to the exact-fp32 kernels
+        and the mode's name would misstate what ran, so the engine refuses it up front (vissm_flow_kernel_precision).
+        bf16x2f (a host mode: forward at VISSM_PREC_BF16X2, backward bf16) stays available on every shape: where the
+        split-weight forward does not cover it (the three-hidden-layer families) the forward runs the exact-fp32
+        kernels -- never less precise than asked -- and the backward the bf16 kernels."""
+        if self.precision != _lib.VISSM_PREC_BF16X2:
             return
         md = self.mdef
         s = 2 if md.D == 2 else 1
@@ -413,9 +416,9 @@ class Engine:
                               n_win=1, precision=_lib.VISSM_PREC_BF16X2)
             if kernel_precision(shape) != _lib.VISSM_PREC_BF16X2:
                 raise ValueError(
-                    f"precision bf16x2 / bf16x2f runs on the split-weight matrix-core kernels only (one hidden layer, "
+                    f"precision bf16x2 runs on the split-weight matrix-core kernels only (one hidden layer, "
                     f"kernel_len <= 32); {md.family} with {fl.spec.n_hidden} hidden layers and kernel_len {md.k} "
-                    "is not covered: use fp32, bf16 or bf16x3")
+                    "is not covered: use fp32, bf16, bf16x3 or bf16x2f")
             L -= md.k
 
     # ---- batches ----
