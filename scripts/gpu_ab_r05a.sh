@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/r05a; mkdir -p "$OUT"; export TMPDIR=/tmp
 echo "== elbo A/B"; date
-ROUNDS=2 timeout -k 10 400 bash scripts/ab_elbo.sh abl/lib_base.so abl/lib_noslp.so abl/lib_kv8.so > "$OUT/ab_elbo.log" 2>&1 || { tail -20 "$OUT/ab_elbo.log"; exit 2; }
+ROUNDS=2 timeout -k 10 400 bash scripts/ab_elbo.sh abl/lib_base.so abl/lib_noslp.so abl/lib_kv8.so abl/lib_kv8noslp.so > "$OUT/ab_elbo.log" 2>&1 || { tail -20 "$OUT/ab_elbo.log"; exit 2; }
 cat "$OUT/ab_elbo.log"
 echo "== step A/B: shared head backward (base) vs per-sample (hs0), 16-byte du stores vs dword (dux4off)"; date
 OUT=$OUT ROUNDS=2 STEPS=8 timeout -k 10 900 bash scripts/ab_step.sh abl/lib_base.so abl/lib_hs0.so abl/lib_dux4off.so \

@@ -133,8 +133,8 @@ def test_model_elbo_kernels_match_oracle(model, M, n_win):
 @pytest.mark.parametrize("model", ["ar", "lv", "sv", "fhn"])
 def test_one_pass_equals_forward_and_backward(model, M, n_win):
     """vissm_elbo_fwd_grad (values, dz and dtheta from one read of z; the training step's ELBO for every model)
-    against the two launches it replaces: the values to fp32 summation order, dz bitwise (the same per-element
-    arithmetic), dtheta to summation order; and against the float64 oracle's values and autograd at the
+    against the two launches it replaces: the values to fp32 summation order, dz to rounding (the same per-element
+    formulas; the compiler contracts them into FMAs differently in the two kernels), dtheta to summation order; and against the float64 oracle's values and autograd at the
     two-launch bars (test above)."""
     from viforssms_amd import _lib
     from viforssms_amd.ops import ElboFeeds, elbo_terms, elbo_values_grad
@@ -176,8 +176,8 @@ def test_one_pass_equals_forward_and_backward(model, M, n_win):
     if model != "sv":
         assert rel(o1, obs) < 2e-6
     if model == "lv":
-        assert float((e1 - ex).abs().max()) <= 2e-6 * float(ex.abs().max()) + 1e-6
-    assert torch.equal(dz1, zd.grad), float((dz1 - zd.grad).abs().max())
+        assert float((e1 - ex.detach()).abs().max()) <= 2e-6 * float(ex.detach().abs().max()) + 1e-6
+    assert rel(dz1, zd.grad) < 1e-6, rel(dz1, zd.grad)
     assert rel(dth1, thd.grad) < 1e-6
     if model != "ar":
         zr, thr = d["z"].clone().requires_grad_(True), d["theta"].clone().requires_grad_(True)
