@@ -36,15 +36,17 @@ MODES = {
 PRECISION_MODE = {1: "bf16", 17: "bf16x2f", 3: "bf16x2"}
 
 MODE = {}
-# realisation jitter: the kernels round fp32 values whose last bits depend on their accumulation order; a relative
-# perturbation of JITTER[0] (~the fp32 accumulation error) before each rounding draws another realisation of the same
-# rounding model (None: the plain emulation)
-JITTER = [None, None]   # [relative size, torch.Generator]
+# Realisations.  The kernels round the same operands in a scaled domain -- activations and weights carry log2(e)
+# (flow_v5.hip: ELU on v_exp_f32), the theta fold splits its rows -- so their rounding errors are another draw of the
+# same distribution, not the emulation's bit pattern.  Realisation s > 0 rounds every operand tensor as bf16(c x) / c
+# with c uniform in [1, 2) drawn per rounding (REAL[1] seeded by s): the same rounding model, other error patterns.
+REAL = [False, None]   # [on, torch.Generator]
 
 
 def rb(x):
-    if JITTER[0]:
-        x = x * (1.0 + JITTER[0] * (2.0 * torch.rand(x.shape, generator=JITTER[1], dtype=x.dtype) - 1.0))
+    if REAL[0]:
+        c = 1.0 + float(torch.rand((), generator=REAL[1], dtype=torch.float64))
+        return (x * c).float().bfloat16().double() / c
     return x.float().bfloat16().double()
 
 
@@ -104,11 +106,11 @@ _PLAIN = O.iaf_flow
 
 
 @contextlib.contextmanager
-def emulate(mode, jitter: float = 0.0, seed: int = 0):
+def emulate(mode, realisation: int = 0):
     """Within the block every nma_oracle flow evaluation rounds as precision `mode` ("bf16", "bf16x2f", "bf16x2";
-    a dict of rounding switches; None: exact); jitter > 0: realisation `seed` of the rounding (JITTER)."""
+    a dict of rounding switches; None: exact); realisation > 0: a scaled-domain realisation of the rounding (REAL)."""
     MODE.clear()
-    JITTER[0], JITTER[1] = (jitter, torch.Generator().manual_seed(seed)) if jitter else (None, None)
+    REAL[0], REAL[1] = (True, torch.Generator().manual_seed(realisation)) if realisation else (False, None)
     if mode is not None:
         MODE.update({k: bool(v) for k, v in (MODES[mode] if isinstance(mode, str) else mode).items()})
     O.iaf_flow = iaf_flow_emul if mode is not None else _PLAIN
@@ -117,4 +119,4 @@ def emulate(mode, jitter: float = 0.0, seed: int = 0):
     finally:
         O.iaf_flow = _PLAIN
         MODE.clear()
-        JITTER[0] = JITTER[1] = None
+        REAL[0], REAL[1] = False, None

@@ -11,8 +11,8 @@ forward / recompute activations and weights, the backward chain's weight and gra
 products' activation and gradient operands; split-weight modes keep the weight operand exact), against the exact
 float64 trajectory from the same start, windows and draws as the GPU test.  Adamax turns a rounding into a
 parameter step through the gradient's SIGN where a component is near zero, a discrete event: the plain emulation and
-REALISATIONS - 1 jittered ones (each rounding of a value perturbed by 2^-22 relative first, the size of the fp32
-accumulation-order differences the kernels' values carry) give the envelope (max over realisations) per step.
+REALISATIONS - 1 scaled-domain realisations (oracle/precision_model.py REAL: the kernels round log2(e)-scaled values,
+another draw of the same error distribution) give the envelope (max over realisations) per step.
 
 Output: tests/golden/precision_drift.json, per mode and step: the emulated posterior mean / sd drift (max over
 (theta0, theta1, e^theta2)) and the per-sample ELBO relative error.  The GPU test holds the kernels to
@@ -70,7 +70,7 @@ def run(K=20, p=20, M=5000, k=8, T=5000, realisations=4):
         return _post_stats(th)
 
     def trajectory(mode, seed=0):
-        with emulate(mode, jitter=2.0 ** -22 if seed else 0.0, seed=seed):
+        with emulate(mode, realisation=seed):
             P = P0
             S = [(torch.zeros_like(t), torch.zeros_like(t)) for t in O.param_leaves(P)]
             rec = []

@@ -19,11 +19,16 @@ DEV = "cuda:0"
 
 
 def _check(res, elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2):
-    print({k: v for k, v in res.items() if k != "per_param"})
+    """param_tol: one bar for every variable, or a dict of per-variable bars (emulated_tol)."""
+    print({k: v for k, v in res.items() if k not in ("per_param", "emul")})
     assert res["finite"], res
     assert res["elbo_rel_err"] < elbo_tol, res
     assert res["grad_rel_err"] < grad_tol, res
-    assert res["grad_max_param_err"] < param_tol, (res["worst_param"], res["grad_max_param_err"])
+    if isinstance(param_tol, dict):
+        bad = {n: (e, param_tol[n]) for n, e in res["per_param"].items() if not e < param_tol[n]}
+        assert not bad, bad
+    else:
+        assert res["grad_max_param_err"] < param_tol, (res["worst_param"], res["grad_max_param_err"])
 
 
 @pytest.mark.parametrize("B,M,k,nf,H,nl,fw", [
@@ -68,14 +73,15 @@ def test_family_parity_multi_window(family, k, T, starts):
 # product) keeps the fp32 bar.  The reduced-precision modes (bf16, the BASELINE config's precision; bf16x2f; bf16x2)
 # round their flow products' operands by design, so their bar is derived from that rounding, not from a measurement
 # of the kernels: the oracle is evaluated a second time under the mode's rounding model (oracle/precision_model.py:
-# every operand the kernels round, rounded to bf16, accumulation exact; the plain emulation and jittered realisations)
+# every operand the kernels round, rounded to bf16, accumulation exact; the plain emulation and scaled-domain realisations)
 # and the GPU must stay within EMUL_SAFETY x that emulated error + the fp32 bar (parity_util.emulated_tol).
 BF16X3_TOL = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
 
 
 def _check_emulated(res):
     tol = emulated_tol(res)
-    print("emulated", res["emul"], "->", tol)
+    print("emulated", {k: v for k, v in res["emul"].items() if k != "per_param"},
+          "-> elbo %.2e grad %.2e" % (tol["elbo_tol"], tol["grad_tol"]))
     _check(res, **tol)
 
 

@@ -58,7 +58,7 @@ def _post_stats(theta):
 #  * the reduced-precision modes at the AR-cfg length (BASELINE configs[1]'s window): their flow products round
 #    operands by design and Adamax's normalised steps pass those roundings into the parameters, so their bar comes
 #    from the modes' rounding model, not from a measurement of the kernels: scripts/precision_drift_emul.py runs the
-#    same K steps in float64 under each mode's rounding (oracle/precision_model.py; plain + jittered realisations)
+#    same K steps in float64 under each mode's rounding (oracle/precision_model.py; plain + scaled-domain realisations)
 #    against the exact trajectory (tests/golden/precision_drift.json); after step s the GPU must stay within
 #    EMUL_SAFETY x the envelope's running maximum up to s + the fp32 case's floor (2e-5 on the posterior, 1e-4 on the
 #    ELBO).  At step 0 the parameters are identical, so the ELBO bar is the forward precision's alone.

@@ -47,14 +47,14 @@ def test_emulation_modes():
     assert errs["bf16x2f"][0] < errs["bf16"][0] and errs["bf16x2"][0] == errs["bf16x2f"][0]
     assert errs["bf16x2"][1] < errs["bf16x2f"][1] < errs["bf16"][1]
     assert all(0 < e < 2e-2 for v in errs.values() for e in v)
-    # a jittered realisation moves the errors, not their scale
-    with emulate("bf16", jitter=2.0 ** -22, seed=1):
+    # a scaled-domain realisation moves the errors, not their scale
+    with emulate("bf16", realisation=1):
         ej = _errs(ref, oracle_reference(m, batch, eps, x0))
     assert ej != errs["bf16"] and 0.5 < ej[1] / errs["bf16"][1] < 2.0
 
 
 def test_precision_drift_fixture_reproduces():
-    """The first two steps of the committed fixture's plain (unjittered) realisation, regenerated
+    """The first two steps of the committed fixture's plain realisation, regenerated
     (scripts/precision_drift_emul.py); the envelope is the maximum over the realisations."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
