@@ -30,10 +30,8 @@ struct Args {
 // ---------------------------------------------------------------------------
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-#ifndef VISSM_ELBO_KV
-#define VISSM_ELBO_KV 4
-#endif
-constexpr int kV = VISSM_ELBO_KV;   // times per chunk (A/B builds: VISSM_ELBO_KV=8)
+// times per chunk (8: slower for every model, LV one-pass 0.48 -> 0.55 ms, profiles/r05/ab_elbo.log)
+constexpr int kV = 4;
 constexpr int kSU = 2;  // chunks per lane in flight
 constexpr int kSW = 4;  // trajectories (waves) per 256-thread block
 

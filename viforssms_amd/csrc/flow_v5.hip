@@ -54,8 +54,6 @@
 #ifndef VISSM_ABL_STORES
 #define VISSM_ABL_STORES 0
 #endif
-// du of a full 16-position tile as four 16-byte stores per sample (lanes q = 4i gather q .. q + 3 by DPP row shifts)
-// where the row pitch and the tile start are 4-float aligned (padded flow rows: every middle flow); dword stores else
 
 namespace vissm {
 namespace VISSM_FLOW5_NS {
@@ -1314,23 +1312,11 @@ __global__ __launch_bounds__(NT, 2) void bwd_kernel(KArgs a, const float* __rest
 // ---------------------------------------------------------------------------
 constexpr int NW2 = 8;
 constexpr int NT2 = 64 * NW2;
-// bwd2: the pair's head backward in one pass, one sample per lane-group pair (VISSM_BWD2_HEADSHARE=0: once per sample)
-#ifndef VISSM_BWD2_HEADSHARE
-#define VISSM_BWD2_HEADSHARE 1
-#endif
-#ifndef VISSM_DU_X4
-#define VISSM_DU_X4 1
-#endif
 // lanes 32..63 of v into lanes 0..31 (v_permlane32_swap); lanes 32..63 of the result keep v's
 __device__ __forceinline__ float swap_hi_lo(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
                                                   false, false);
   return __builtin_bit_cast(float, static_cast<unsigned>(r[1]));
-}
-template <int N>
-__device__ __forceinline__ float row_shl_n(float v) {  // lane c <- lane c + N within its row of 16
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
-                                                               0x100 + N, 0xf, 0xf, false));
 }
 constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 // Design decisions (A/B, AR-cfg launches):
@@ -1623,51 +1609,46 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       const bool pv = c < nP;
       float gmu[2], gr[2];
       float lsv[2] = {0.f, 0.f};  // fused variant without the LDS column sums: the output columns' log sigma
-#if VISSM_BWD2_HEADSHARE
-      // Both samples' head backward in one pass: lane groups 0, 1 evaluate sample A's columns and 2, 3 sample B's
-      // (the head MFMA left every column's (mu, r) in all four groups), so the softplus / sigmoid / upstream-gradient
-      // work runs once per pair instead of once per sample; v_permlane32_swap then brings B's (g_mu, g_r) from groups
-      // 2, 3 to 0, 1, where the dZ product's B operand (group 0) and the I_1 image rows (group 1) take them.
-      {
+      if constexpr (FZ) {
+        // Fused last flow: both samples' head backward in one pass: lane groups 0, 1 evaluate sample A's columns and
+        // 2, 3 sample B's (the head MFMA left every column's (mu, r) in all four groups), so the softplus / sigmoid /
+        // AR(1) transition and observation gradient work runs once per pair instead of once per sample;
+        // v_permlane32_swap then brings B's (g_mu, g_r) from groups 2, 3 to 0, 1, where the dZ product's B operand
+        // (group 0) and the I_1 image rows (group 1) take them.  Fused flow 23.8 -> 23.4 ms per AR-cfg launch; the
+        // unfused variants' lighter head gains nothing from it (first flow +0.3 ms, middle +0.0,
+        // profiles/r05/ab_step.log), so they keep the per-sample form below.
         const int hs = g >> 1;                      // the sample of this lane's head work
         const bool hv = hs == 0 || two;             // not the ghost
         const float mu_h = hs ? mu[1] : mu[0], rr_h = hs ? rr[1] : rr[0];
         const float sig_h = softplus_fast(rr_h) + 1e-10f;
         const float uk = uwin[w][hs][c + a.k];
-        float gmu_h, lsv_h = 0.f;
-        if constexpr (FZ) {
-          const float x = uk * sig_h + mu_h;
-          float xp = row_prev(x);
-          const float xn = row_next(x);
-          if (c == 0) xp = hs ? fz_zc[1] : fz_zc[0];
-          const int bl2 = hs ? blv[1] : blv[0];
-          const float th0 = hs ? lane_f(lt0, blv[1]) : lane_f(lt0, blv[0]);
-          const float th1 = hs ? lane_f(lt1, blv[1]) : lane_f(lt1, blv[0]);
-          const float is = hs ? lane_f(lis, blv[1]) : lane_f(lis, blv[0]);
-          const int t = m0 + c;
-          const float fh = (pv && t < fz.M) ? 1.f : 0.f;
-          const float ft = (pv && t >= 1) ? 1.f : 0.f;
-          const float bp = fz_bp * ft;
-          const float zt = fh * (xn - th1 * x - th0) * is;
-          const float zp = ft * (x - th1 * xp - th0) * is;
-          const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
-          gmu_h = hv ? -fz.scale * de : 0.f;
-          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig_h) * kLn2 : 0.f;
-          if ((g & 1) == 0) {  // lane groups 0 (A) and 2 (B)
-            if constexpr (NPR == 1) gwin[w][hs][c] = gmu_h;  // the upstream-gradient window the du section reads
-            if (pv && hv) {
-              if constexpr (!(VISSM_ABL_STORES & 1)) fz.x[static_cast<size_t>(b_lo + bl2) * (fz.M + 1) + t] = x;
-              if constexpr (ZLS) zls[w][bl2][c] += lsg;
-            }
+        const float x = uk * sig_h + mu_h;
+        float xp = row_prev(x);
+        const float xn = row_next(x);
+        if (c == 0) xp = hs ? fz_zc[1] : fz_zc[0];
+        const int bl2 = hs ? blv[1] : blv[0];
+        const float th0 = hs ? lane_f(lt0, blv[1]) : lane_f(lt0, blv[0]);
+        const float th1 = hs ? lane_f(lt1, blv[1]) : lane_f(lt1, blv[0]);
+        const float is = hs ? lane_f(lis, blv[1]) : lane_f(lis, blv[0]);
+        const int t = m0 + c;
+        const float fh = (pv && t < fz.M) ? 1.f : 0.f;
+        const float ft = (pv && t >= 1) ? 1.f : 0.f;
+        const float bp = fz_bp * ft;
+        const float zt = fh * (xn - th1 * x - th0) * is;
+        const float zp = ft * (x - th1 * xp - th0) * is;
+        const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
+        const float gmu_h = hv ? -fz.scale * de : 0.f;
+        const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig_h) * kLn2 : 0.f;
+        if ((g & 1) == 0) {  // lane groups 0 (A) and 2 (B)
+          if constexpr (NPR == 1) gwin[w][hs][c] = gmu_h;  // the upstream-gradient window the du section reads
+          if (pv && hv) {
+            if constexpr (!(VISSM_ABL_STORES & 1)) fz.x[static_cast<size_t>(b_lo + bl2) * (fz.M + 1) + t] = x;
+            if constexpr (ZLS) zls[w][bl2][c] += lsg;
           }
-          if constexpr (!ZLS) lsv_h = (pv && hv) ? lsg : 0.f;
-          if ((lane & 31) == PO - 1 && (nP == PO || discard) && hv) zcar[w][bl2] = x;
-        } else {
-          gmu_h = pv ? gwin[w][hs][c] : 0.f;
         }
-        const float dl = FZ ? -fz.scale : (hs ? lane_f(ldl, blv[1]) : lane_f(ldl, blv[0]));
+        if ((lane & 31) == PO - 1 && (nP == PO || discard) && hv) zcar[w][bl2] = x;
         float dsig = gmu_h * uk;
-        if (pv && hv && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig_h);
+        if (pv && hv && t0 + c >= a.Lout - a.n_logsig) dsig += -fz.scale * rcp_f(sig_h);
         const float gr_h = dsig * sigmoid_fast(rr_h);
         if ((g & 1) == 0) {
           if constexpr (NPR == 2) {
@@ -1680,74 +1661,47 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         gr[0] = gr_h;
         gmu[1] = swap_hi_lo(gmu_h);
         gr[1] = swap_hi_lo(gr_h);
-        if constexpr (FZ && !ZLS) {
+        if constexpr (!ZLS) {
+          const float lsv_h = (pv && hv) ? lsg : 0.f;
           lsv[0] = lsv_h;
           lsv[1] = swap_hi_lo(lsv_h);
         }
-      }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        if (g == 1) {
-          const int off = timg_off(c, 4 * 3 + 1);
-          *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
-        }
-      }
-#else
-      float sig[2];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        sig[cb] = softplus_fast(rr[cb]) + 1e-10f;
-        if constexpr (FZ) {
-          const float x = uwin[w][cb][c + a.k] * sig[cb] + mu[cb];
-          float xp = row_prev(x);
-          const float xn = row_next(x);
-          if (c == 0) xp = fz_zc[cb];
-          const int bl2 = blv[cb];
-          const float th0 = lane_f(lt0, bl2), th1 = lane_f(lt1, bl2), is = lane_f(lis, bl2);
-          const int t = m0 + c;
-          const float fh = (pv && t < fz.M) ? 1.f : 0.f;
-          const float ft = (pv && t >= 1) ? 1.f : 0.f;
-          const float bp = fz_bp * ft;
-          const float zt = fh * (xn - th1 * x - th0) * is;
-          const float zp = ft * (x - th1 * xp - th0) * is;
-          const float de = th1 * zt * is - zp * is - bp * (x - fz_yp) * (fz.iosd * fz.iosd);
-          gmu[cb] = (cb == 0 || two) ? -fz.scale * de : 0.f;
-          const float lsg = (t0 + c >= a.Lout - a.n_logsig) ? __builtin_amdgcn_logf(sig[cb]) * kLn2 : 0.f;
-          if (g == 0) {
-            if constexpr (NPR == 1) gwin[w][cb][c] = gmu[cb];  // the upstream-gradient window the du section reads
-            if (pv && (cb == 0 || two)) {
-              if constexpr (!(VISSM_ABL_STORES & 1)) fz.x[static_cast<size_t>(bv[cb]) * (fz.M + 1) + t] = x;
-              if constexpr (ZLS) zls[w][bl2][c] += lsg;
-            }
+        for (int cb = 0; cb < 2; ++cb) {
+          if (g == 1) {  // G = (g_mu, g_r) into the I_1 image's padding rows 53, 54 (as below)
+            const int off = timg_off(c, 4 * 3 + 1);
+            *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
           }
-          if constexpr (!ZLS) lsv[cb] = (pv && (cb == 0 || two)) ? lsg : 0.f;
-          if (lane == PO - 1 && (nP == PO || discard) && (cb == 0 || two)) zcar[w][bl2] = x;
-        } else {
+        }
+      } else {
+        float sig[2];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          sig[cb] = softplus_fast(rr[cb]) + 1e-10f;
           gmu[cb] = pv ? gwin[w][cb][c] : 0.f;
         }
-      }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const float dl = FZ ? -fz.scale : lane_f(ldl, blv[cb]);
-        float dsig = gmu[cb] * uwin[w][cb][c + a.k];
-        if (pv && (cb == 0 || two) && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig[cb]);
-        gr[cb] = dsig * sigmoid_fast(rr[cb]);
-        if (g == 0) {
-          if constexpr (NPR == 2) {
-            if constexpr (DU) gwin[w][cb][c] = gmu[cb] * sig[cb];  // (after the reads of g_mu above: LDS order)
-          } else {
-            gsc[w][cb][c] = sig[cb];
+        for (int cb = 0; cb < 2; ++cb) {
+          const float dl = lane_f(ldl, blv[cb]);
+          float dsig = gmu[cb] * uwin[w][cb][c + a.k];
+          if (pv && (cb == 0 || two) && t0 + c >= a.Lout - a.n_logsig) dsig += dl * rcp_f(sig[cb]);
+          gr[cb] = dsig * sigmoid_fast(rr[cb]);
+          if (g == 0) {
+            if constexpr (NPR == 2) {
+              if constexpr (DU) gwin[w][cb][c] = gmu[cb] * sig[cb];  // (after the reads of g_mu above: LDS order)
+            } else {
+              gsc[w][cb][c] = sig[cb];
+            }
+          }
+          // the head gradient G = (g_mu, g_r) at p = c into the I_1 image's padding rows 53, 54 (register (3, 1),
+          // (3, 2) of lane group 1; unit 49 in row 52 rewritten unchanged): dW_head = I_1 G^T then takes both
+          // operands from this one image, before the dZ image overwrites its slot
+          if (g == 1) {
+            const int off = timg_off(c, 4 * 3 + 1);
+            *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
           }
         }
-        // the head gradient G = (g_mu, g_r) at p = c into the I_1 image's padding rows 53, 54 (register (3, 1),
-        // (3, 2) of lane group 1; unit 49 in row 52 rewritten unchanged): dW_head = I_1 G^T then takes both
-        // operands from this one image, before the dZ image overwrites its slot
-        if (g == 1) {
-          const int off = timg_off(c, 4 * 3 + 1);
-          *reinterpret_cast<u2*>(im1 + cb * P * HP + off) = u2{cvt2(X[cb][3][0], gmu[cb]), cvt2(gr[cb], X[cb][3][3])};
-        }
       }
-#endif
       fence2<FZ>();
       // dW_head[h][o] += sum over both samples' positions of I_1[h][p] G[o][p] (K = 32): block 3 of the same
       // fragments is the B operand (its columns 5, 6 are the G rows)
@@ -1935,17 +1889,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           if (oq2 >= 0 && oq2 < nP) v += NPR == 2 ? gwin[w][cbq][oq2] : gwin[w][cbq][oq2] * gsc[w][cbq][oq2];
           if (q < a.k) v += carry[w][blq][q];
         }
-        float* const dur = du + static_cast<size_t>(b_lo + blq) * a.pL + t0;
-        if (!FZ && VISSM_DU_X4 && nP == P && ((a.pL | t0) & 3) == 0) {  // wave-uniform
-          const float v1 = row_shl_n<1>(v), v2 = row_shl_n<2>(v), v3 = row_shl_n<3>(v);
-          if (act) {
-            if (q < P) {
-              if ((q & 3) == 0 && !(VISSM_ABL_STORES & 2)) *reinterpret_cast<f4*>(dur + q) = f4{v, v1, v2, v3};
-            } else {
-              carry[w][blq][q - P] = v;
-            }
-          }
-        } else if (act) {
+        // (16-byte du stores of full aligned tiles -- four lanes' values gathered by DPP row shifts -- measured 0.2 ms
+        // slower per middle-flow launch and no fewer PMC write bytes (4.05 vs 4.07 GB), profiles/r05/ab_step.log)
+        if (act) {
+          float* const dur = du + static_cast<size_t>(b_lo + blq) * a.pL + t0;
           if (q < nP) {
             if constexpr (!(VISSM_ABL_STORES & 2)) dur[q] = v;
           } else {
