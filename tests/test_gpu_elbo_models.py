@@ -128,7 +128,9 @@ def test_model_elbo_kernels_match_oracle(model, M, n_win):
     assert rel(thd.grad, thr.grad) < 1e-4
 
 
-@pytest.mark.parametrize("M", [1, 3, 4, 5, 9, 50, 1001, 2000])
+# M + 1 elements in chunks of 4: no chunk (M < 3), one chunk (element-wise only), the neighbour-exchange loop with a
+# partial iteration, exactly one / two full iterations of 64 chunks (the deferred lane 63), one chunk past them
+@pytest.mark.parametrize("M", [1, 3, 4, 5, 8, 9, 50, 258, 259, 260, 515, 519, 1001, 2000])
 @pytest.mark.parametrize("n_win", [1, 3])
 @pytest.mark.parametrize("model", ["ar", "lv", "sv", "fhn"])
 def test_one_pass_equals_forward_and_backward(model, M, n_win):

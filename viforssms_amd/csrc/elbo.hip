@@ -34,6 +34,9 @@ typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 constexpr int kV = 4;
 constexpr int kSU = 2;  // chunks per lane in flight
 constexpr int kSW = 4;  // trajectories (waves) per 256-thread block
+#ifndef VISSM_ELBO_ONEPASS_NB
+#define VISSM_ELBO_ONEPASS_NB 1   // vissm_elbo_fwd_grad's LV / SV / FHN kernel: neighbour exchange (0: chunk-local)
+#endif
 
 __device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 
@@ -604,6 +607,276 @@ __global__ __launch_bounds__(256) void stream_bwd_kernel(Args a, const float* __
 }
 
 // ---------------------------------------------------------------------------
+// One pass with neighbour exchange (vissm_elbo_fwd_grad, LV / SV / FHN).  stream_bwd_kernel evaluates kV + 2 states and
+// kV + 1 transitions per chunk of kV elements (each chunk recomputes its neighbours' edge states and the transition
+// across its left edge); here every state and transition is evaluated exactly once: lane l of iteration i owns chunk
+// c = 1 + 64 i + l (elements t0 = kV c .. t0 + kV - 1), evaluates its kV states and the kV transitions ENTERING its
+// elements (T_{t0-1} .. T_{t0+kV-2}, T_e: x_e -> x_{e+1}), takes x_{t0-1} from lane l - 1 by a DPP wave shift (lane 0:
+// the previous iteration's lane 63, or element kV - 1 before the loop) and the head gradient of its last element --
+// T_{t0+kV-1}, lane l + 1's first transition -- by the opposite shift.  The lane whose right neighbour is not in this
+// iteration (lane 63, or the last chunk's lane) keeps that element pending: the next iteration's lane 0 (or the
+// element-wise tail after the loop) supplies the missing head through v_readlane, then that chunk is stored.  Elements
+// [0, kV) and [kV nfull, M] run element-wise as in stream_bwd_kernel, with transition counts chosen so that every
+// transition's log-density and theta gradient enters the sums once.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_shr1(float v) {  // lane l <- lane l - 1 (lane 0 keeps v)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_shl1(float v) {  // lane l <- lane l + 1 (lane 63 keeps v)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_val(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float* __restrict__ z,
+                                                             const float* __restrict__ theta,
+                                                             const float* __restrict__ g_sde,
+                                                             const float* __restrict__ g_obs,
+                                                             const float* __restrict__ g_ex, float* __restrict__ dz,
+                                                             float* __restrict__ dtheta, Vals vo) {
+  using Dv = Dev<MODEL>;
+  constexpr int ZD = Dv::ZD, P = Dv::P;
+  const int lane = threadIdx.x & 63;
+  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kSW + (threadIdx.x >> 6));
+  if (b >= a.B) return;  // wave-uniform
+  const int M = a.M;
+  const int w = a.d.win ? a.d.win[b] : 0;
+  Dv m;
+  m.init(a, theta + static_cast<size_t>(b) * P, w);
+  const float* zb = z + static_cast<size_t>(b) * ZD * (M + 1);
+  float* dzb = dz + static_cast<size_t>(b) * ZD * (M + 1);
+  const float gs = g_sde ? g_sde[b] : 0.f;
+  const float go = (Dv::kObs && g_obs) ? g_obs[b] : 0.f;
+  const float ge = (Dv::kExtra && g_ex) ? g_ex[b] : 0.f;
+  const float cgo = -go / (Dv::kSd * Dv::kSd);
+  constexpr float isd = 1.f / Dv::kSd;
+  float acc[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) acc[i] = 0.f;
+  float s_lp = 0.f, s_q = 0.f, s_b = 0.f, s_e = 0.f;
+  // a transition's log-density and theta gradient into the sums (on: a 0 / 1 weight, lanes that own it)
+  auto count = [&](const em::TG& r, float on) {
+    s_lp += on * r.lp;
+#pragma unroll
+    for (int i = 0; i < P; ++i) acc[i] += on * r.gth[i];
+  };
+  // the obs row e - 1 observing x_e (e >= 1): gradient into g, value into the sums
+  auto obs_g = [&](const St& s, float y0, float y1, float b0, float b1, float* g, float on) {
+    if constexpr (Dv::kObs) {
+      const float d0 = s.x[0] - y0, d1 = s.x[1] - y1;
+      g[0] += cgo * b0 * d0;
+      g[1] += cgo * b1 * d1;
+      s_q += on * (b0 * (d0 * isd) * (d0 * isd) + b1 * (d1 * isd) * (d1 * isd));
+      s_b += on * (b0 + b1);
+    }
+  };
+  // dz of element s from its state gradient g (+ the ILDJ term observing it, e >= 1)
+  auto dz_of = [&](const St& s, const float* g, bool ildj, float on, float* o) {
+    if constexpr (ZD == 2) {
+      o[0] = g[0] * s.j[0];
+      o[1] = g[1] * s.j[1];
+      if constexpr (Dv::kExtra) {
+        if (ildj) {
+          o[0] += ge * s.dil[0];
+          o[1] += ge * s.dil[1];
+          s_e += on * (s.il[0] + s.il[1]);
+        }
+      }
+    } else {
+      o[0] = g[1] * s.j[1];
+    }
+  };
+  const int nfull = (M + 1) / kV;  // chunks whose kV elements all exist (elements 0 .. M)
+  // ---- the chunk loop: chunks 1 .. nfull - 1 ----
+  float pend[ZD * kV];             // the deferred chunk (meaningful in lane pl only)
+  float pg[2] = {0.f, 0.f}, pj[2] = {0.f, 0.f};  // its last element's state gradient (without the head) and d x / d z
+  int pl = -1, pt0 = 0;            // the deferring lane and its chunk's first element (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < ZD * kV; ++i) pend[i] = 0.f;
+  float xc0 = 0.f, xc1 = 0.f;      // x of element t0 - 1 for lane 0
+  if (nfull >= 2) {
+    const St s3 = m.state(zb, kV - 1);
+    xc0 = s3.x[0];
+    xc1 = s3.x[1];
+  }
+  for (int c0 = 1; c0 < nfull; c0 += 64) {
+    const int c = c0 + lane;
+    const bool act = c < nfull;
+    const float on = act ? 1.f : 0.f;
+    const int t0 = kV * (act ? c : nfull - 1);   // idle lanes of the last iteration evaluate the last chunk, unused
+    St st[kV];
+    m.template states<kV>(zb, t0, st);
+    float y[2][kV], bb[2][kV];
+    if constexpr (Dv::kObs) {  // rows t0 - 1 .. t0 + kV - 2 observe x_{t0} .. x_{t0+kV-1}
+      ldn<kV>(m.ob + t0 - 1, y[0]);
+      ldn<kV>(m.ob + M + t0 - 1, y[1]);
+      ldn<kV>(m.bn + t0 - 1, bb[0]);
+      ldn<kV>(m.bn + M + t0 - 1, bb[1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kV; ++j) y[0][j] = y[1][j] = bb[0][j] = bb[1][j] = 0.f;
+    }
+    // x_{t0-1}: lane l - 1's last state; lane 0: the carry
+    St left;
+    const float sh0 = wave_shr1(st[kV - 1].x[0]), sh1 = wave_shr1(st[kV - 1].x[1]);  // every lane issues the shift
+    left.x[0] = lane == 0 ? xc0 : sh0;
+    left.x[1] = lane == 0 ? xc1 : sh1;
+    // the transitions entering the chunk's elements
+    em::TG tr[kV];
+    tr[0] = m.trans(left, st[0]);
+#pragma unroll
+    for (int j = 1; j < kV; ++j) tr[j] = m.trans(st[j - 1], st[j]);
+#pragma unroll
+    for (int j = 0; j < kV; ++j) count(tr[j], on);
+    // the head of the chunk's last element: lane l + 1's first transition
+    const float hn0 = wave_shl1(tr[0].gh[0]), hn1 = wave_shl1(tr[0].gh[1]);
+    // the previous iteration's deferred chunk: its head is this iteration's lane-0 first transition
+    if (pl >= 0) {
+      const float h0 = lane_val(tr[0].gh[0], 0), h1 = lane_val(tr[0].gh[1], 0);
+      if (lane == pl) {
+        const float g[2] = {pg[0] + gs * h0, pg[1] + gs * h1};
+        if constexpr (ZD == 2) {
+          pend[ZD * (kV - 1)] += g[0] * pj[0];
+          pend[ZD * (kV - 1) + 1] += g[1] * pj[1];
+        } else {
+          pend[kV - 1] += g[1] * pj[1];
+        }
+#pragma unroll
+        for (int i = 0; i < ZD * kV; i += 4)
+          *reinterpret_cast<f4u*>(dzb + ZD * pt0 + i) = f4u{pend[i], pend[i + 1], pend[i + 2], pend[i + 3]};
+      }
+    }
+    // elements t0 .. t0 + kV - 1
+    const int last_c = min(nfull - 1, c0 + 63);
+    const int dl = last_c - c0;                   // the lane that defers its last element (wave-uniform)
+    float o[ZD * kV];
+    float glast[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kV; ++j) {
+      float g[2] = {gs * tr[j].gt[0], gs * tr[j].gt[1]};        // tail: T_{e-1}
+      if (j + 1 < kV) {                                            // head: T_e
+        g[0] += gs * tr[j + 1].gh[0];
+        g[1] += gs * tr[j + 1].gh[1];
+      }
+      obs_g(st[j], y[0][j], y[1][j], bb[0][j], bb[1][j], g, on);
+      if (j + 1 == kV) {
+        glast[0] = g[0];
+        glast[1] = g[1];
+        if (lane != dl) {
+          g[0] += gs * hn0;
+          g[1] += gs * hn1;
+        }
+      }
+      dz_of(st[j], g, true, on, o + ZD * j);
+    }
+    if (act && lane != dl) {
+#pragma unroll
+      for (int i = 0; i < ZD * kV; i += 4)
+        *reinterpret_cast<f4u*>(dzb + ZD * t0 + i) = f4u{o[i], o[i + 1], o[i + 2], o[i + 3]};
+    }
+    // defer lane dl's chunk: its dz without the last element's head, that element's state gradient and d x / d z
+    if (lane == dl) {
+#pragma unroll
+      for (int i = 0; i < ZD * kV; ++i) pend[i] = o[i];
+      if constexpr (ZD == 2) {
+        pend[ZD * (kV - 1)] -= glast[0] * st[kV - 1].j[0];
+        pend[ZD * (kV - 1) + 1] -= glast[1] * st[kV - 1].j[1];
+      } else {
+        pend[kV - 1] -= glast[1] * st[kV - 1].j[1];
+      }
+      pg[0] = glast[0];
+      pg[1] = glast[1];
+      pj[0] = st[kV - 1].j[0];
+      pj[1] = st[kV - 1].j[1];
+    }
+    pl = dl;
+    pt0 = kV * last_c;
+    xc0 = lane_val(st[kV - 1].x[0], 63);
+    xc1 = lane_val(st[kV - 1].x[1], 63);
+  }
+  // ---- element-wise tail: elements [0, kV) and [kV nfull, M] ----
+  const int lo_end = nfull >= 1 ? kV : M + 1;
+  const int nrest = lo_end + (nfull >= 1 ? (M + 1 - kV * nfull) : 0);
+  float hpend0 = 0.f, hpend1 = 0.f;   // the head of element kV nfull - 1 (the deferred chunk's last element)
+  for (int r0 = 0; r0 < nrest; r0 += 64) {
+    const int r = r0 + lane;
+    const bool on_r = r < nrest;
+    const int t = !on_r ? 0 : (r < lo_end ? r : kV * nfull + (r - lo_end));
+    const St sc = m.state(zb, t);
+    float g[2] = {0.f, 0.f};
+    if (on_r && t < M) {
+      const em::TG h = m.trans(sc, m.state(zb, t + 1));
+      g[0] += gs * h.gh[0];
+      g[1] += gs * h.gh[1];
+      // counted here unless the chunk loop counted it (T_{kV-1}: chunk 1's first transition)
+      if (!(t == kV - 1 && nfull >= 2)) count(h, 1.f);
+    }
+    if (on_r && t >= 1) {
+      const em::TG tl = m.trans(m.state(zb, t - 1), sc);
+      g[0] += gs * tl.gt[0];
+      g[1] += gs * tl.gt[1];
+      if (t == kV * nfull && nfull >= 2) {   // T_{kV nfull - 1}: the deferred element's head, counted once here
+        count(tl, 1.f);
+        hpend0 = tl.gh[0];
+        hpend1 = tl.gh[1];
+      }
+      if constexpr (Dv::kObs)
+        obs_g(sc, m.ob[t - 1], m.ob[M + t - 1], m.bn[t - 1], m.bn[M + t - 1], g, 1.f);
+    }
+    float o[ZD];
+    dz_of(sc, g, on_r && t >= 1, on_r ? 1.f : 0.f, o);
+    if (on_r) {
+      if constexpr (ZD == 2) {
+        dzb[2 * t] = o[0];
+        dzb[2 * t + 1] = o[1];
+      } else {
+        dzb[t] = o[0];
+      }
+    }
+  }
+  // the last deferred chunk: its head from the tail's element kV nfull (lane lo_end), or none (kV nfull - 1 == M)
+  if (pl >= 0) {
+    float h0 = 0.f, h1 = 0.f;
+    if (kV * nfull <= M) {
+      h0 = lane_val(hpend0, lo_end % 64);
+      h1 = lane_val(hpend1, lo_end % 64);
+    }
+    if (lane == pl) {
+      if constexpr (ZD == 2) {
+        pend[ZD * (kV - 1)] += (pg[0] + gs * h0) * pj[0];
+        pend[ZD * (kV - 1) + 1] += (pg[1] + gs * h1) * pj[1];
+      } else {
+        pend[kV - 1] += (pg[1] + gs * h1) * pj[1];
+      }
+#pragma unroll
+      for (int i = 0; i < ZD * kV; i += 4)
+        *reinterpret_cast<f4u*>(dzb + ZD * pt0 + i) = f4u{pend[i], pend[i + 1], pend[i + 2], pend[i + 3]};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const double s = wave_sum(static_cast<double>(acc[i]));
+    if (lane == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(gs * s);
+  }
+  const double r_lp = wave_sum(static_cast<double>(s_lp));
+  const double r_q = wave_sum(static_cast<double>(s_q));
+  const double r_b = wave_sum(static_cast<double>(s_b));
+  const double r_e = wave_sum(static_cast<double>(s_e));
+  if (lane == 0) {
+    vo.sde[b] = static_cast<float>(r_lp);
+    if (vo.obs)
+      vo.obs[b] = Dv::kObs ? static_cast<float>(-0.5 * r_q + r_b * (-std::log(static_cast<double>(Dv::kSd)) -
+                                                                    0.5 * kLog2Pi))
+                           : 0.f;
+    if (vo.extra) vo.extra[b] = static_cast<float>(r_e);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // AR(1) streaming path (the BASELINE configs): the same terms as Model<AR> above, laid out for
 // HBM: each thread owns V = 4 consecutive times and reads its z span with one 16-byte load (the
 // rows are only dword-aligned: M + 1 floats per sample), the window's obs / obs_bin with one
@@ -946,9 +1219,15 @@ int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const
       hipLaunchKernelGGL(ar_elbo_bwd_kernel<true>, dim3((d->B + kArW - 1) / kArW), blk, 0, st, a, z, theta, g_sde,
                          g_obs, dz, dtheta, vo);
       break;
+#if VISSM_ELBO_ONEPASS_NB
+    case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_SV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    default: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+#else
     case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_SV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
     default: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_FHN, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+#endif
   }
   VISSM_CHECK_LAUNCH("elbo_fwd_grad");
   // algorithmic bytes: z read once, dz written, theta / dtheta, the upstream gradients and the three sums
