@@ -467,6 +467,8 @@ def measure(args, ctx, dev, parity_line: bool):
                                  "elbo_fwd_kernel (log-densities: reads z)",
              _lib.PROF_ELBO_BWD: ("elbo_bwd_kernel (reads z, writes the per-sample theta gradient only: the fused "
                                   "last flow differentiated through z itself)") if fused else
+                                 ("elbo_onepass_kernel (values, dz and dtheta from one read of z: reads z, writes dz; "
+                                  "vissm_elbo_fwd_grad)") if model.engine.onepass_ok() else
                                  "elbo_bwd_kernel (reads z, writes dz)",
              _lib.PROF_NORMAL: "normal_base_kernel (Philox base noise: writes eps)"}
     streaming = []

@@ -229,6 +229,10 @@ typedef struct {
   const float* mask;      /* LV [n_win][2][M+1]; SV [n_win][M+1]; else NULL */
   const float* shift;     /* same shape as mask */
   const float* dim_one;   /* SV observed coordinate [n_win][M+1]; else NULL */
+  const int32_t* plain_from; /* LV / SV, optional [n_win]: from this element on, the window's mask is 1 and its
+                                shift 0 (the state is softplus(z) / z itself: the reference's windows pin x_0 only,
+                                lotka_volterra_partial.py:381-384, SV_dense.py:322-328); NULL: mask / shift read
+                                everywhere.  vissm_elbo_fwd_grad skips their loads and the general transform there. */
 } VissmElboData;
 
 int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data,

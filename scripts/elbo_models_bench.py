@@ -55,6 +55,14 @@ def main():
         lib = _lib.load()
         d = ElboDesc(mid, B, M, 1, float(dt), 1.0)
         data = feeds.cdata()
+        pdata = None
+        if feeds.mask is not None:   # the same feeds with the plain-span table (VissmElboData.plain_from)
+            from dataclasses import replace
+            from viforssms_amd.features import plain_from_table
+            mk, sh = feeds.mask[0].double().cpu().numpy(), feeds.shift[0].double().cpu().numpy()
+            pf = torch.as_tensor(plain_from_table(mk, sh, M), device=dev)
+            pfeeds = replace(feeds, plain_from=pf)
+            pdata = pfeeds.cdata()
         st = _lib.stream_handle(dev)
         sde, obs, ex = (torch.empty(B, device=dev) for _ in range(3))
         gs = torch.ones(B, device=dev)
@@ -68,8 +76,12 @@ def main():
             "one": lambda: check(lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(data), ptr(z), ptr(th),
                                                          ptr(gs), ptr(gs), ptr(gs), ptr(sde), ptr(obs), ptr(ex),
                                                          ptr(dz), ptr(dth), st), "one"),
+            "one_plain": lambda: check(lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(pdata), ptr(z), ptr(th),
+                                                               ptr(gs), ptr(gs), ptr(gs), ptr(sde), ptr(obs), ptr(ex),
+                                                               ptr(dz), ptr(dth), st), "one_plain"),
         }
-        kinds = [k for k in ("fwd", "bwd", "one") if k != "one" or hasattr(lib, "vissm_elbo_fwd_grad")]
+        kinds = ["fwd", "bwd"] + (["one"] if hasattr(lib, "vissm_elbo_fwd_grad") else [])
+        kinds += ["one_plain"] if pdata is not None and "one" in kinds else []
         ts = {k: [] for k in kinds}
         for _ in range(rounds):
             for kind in kinds:
@@ -90,6 +102,9 @@ def main():
             o = min(ts["one"])
             out[model].update(one_ms=round(o, 4), one_frac=round(2 * zb / (o * 1e-3) / 8e12, 3),
                               two_launch_ms=round(f + b, 4))
+        if "one_plain" in ts:
+            o = min(ts["one_plain"])
+            out[model].update(one_plain_ms=round(o, 4), one_plain_frac=round(2 * zb / (o * 1e-3) / 8e12, 3))
     print(json.dumps(out))
 
 

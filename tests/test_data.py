@@ -107,6 +107,42 @@ def test_sv_table_shapes():
     assert f["dim_one"].shape == (2, 53) and np.allclose(f["dim_one"][1], obs[52:105])
 
 
+def _plain_from_brute(mask, shift):
+    """per window: one past the last element with mask != 1 or shift != 0 in any row, 0 when none"""
+    out = []
+    for m, s in zip(mask, shift):
+        m, s = np.atleast_2d(m), np.atleast_2d(s)
+        bad = np.where(((m != 1.0) | (s != 0.0)).any(0))[0]
+        out.append(int(bad[-1]) + 1 if bad.size else 0)
+    return out
+
+
+def test_plain_from_table():
+    """features.plain_from_table (VissmElboData.plain_from) == the per-window definition over the FeatureTable's own
+    mask / shift feeds: the reference tables (only window 0 pins x_0) and tables with dirty entries anywhere."""
+    obs, ob, tt = data.load_lv()
+    tab = features.lv_table(obs, ob, tt, np.array([100.0, 100.0]), 50.0, 0.1, 500, 3, 20, 50, 10)
+    starts = np.arange(0, 451)
+    f = tab.feeds(starts)
+    pf = features.plain_from_table(tab.extra["mask_vals"], tab.extra["shift_vals"], tab.M)
+    assert pf.dtype == np.int32 and pf.shape == (451,)
+    assert pf.tolist() == _plain_from_brute(f["mask"], f["shift"])
+    assert pf[0] == 1 and not pf[1:].any()
+    rng = np.random.default_rng(3)
+    for D in (1, 2):
+        for trial in range(20):
+            L, M = int(rng.integers(2, 60)), int(rng.integers(0, 20))
+            M = min(M, L - 1)
+            mv = np.ones((D, L))
+            sv = np.zeros((D, L))
+            for _ in range(int(rng.integers(0, 4))):
+                mv[int(rng.integers(0, D)), int(rng.integers(0, L))] = rng.choice([0.0, 0.5])
+                sv[int(rng.integers(0, D)), int(rng.integers(0, L))] = rng.choice([0.0, 3.0])
+            pf = features.plain_from_table(mv if D == 2 else mv[0], sv if D == 2 else sv[0], M)
+            wins = [(mv[:, s:s + M + 1], sv[:, s:s + M + 1]) for s in range(L - M)]
+            assert pf.tolist() == _plain_from_brute([w[0] for w in wins], [w[1] for w in wins])
+
+
 # --- LV / FHN / SV host feeds against the oracle's independent restatement (bit-exact) ---------
 @pytest.mark.parametrize("family", ["lv", "fhn"])
 @pytest.mark.parametrize("n,k,M,fw,starts", [(3, 20, 50, 10, [0, 50, 450, 50]), (2, 4, 24, 3, [0, 24, 48, 456]),

@@ -128,9 +128,9 @@ def test_model_elbo_kernels_match_oracle(model, M, n_win):
     assert rel(thd.grad, thr.grad) < 1e-4
 
 
-# M + 1 elements in chunks of 4: no chunk (M < 3), one chunk (element-wise only), the neighbour-exchange loop with a
+# M + 1 elements in chunks of 4 (LV: 2): no chunk, one chunk (element-wise only), the neighbour-exchange loop with a
 # partial iteration, exactly one / two full iterations of 64 chunks (the deferred lane 63), one chunk past them
-@pytest.mark.parametrize("M", [1, 3, 4, 5, 8, 9, 50, 258, 259, 260, 515, 519, 1001, 2000])
+@pytest.mark.parametrize("M", [1, 3, 4, 5, 8, 9, 50, 128, 129, 130, 258, 259, 260, 515, 519, 1001, 2000])
 @pytest.mark.parametrize("n_win", [1, 3])
 @pytest.mark.parametrize("model", ["ar", "lv", "sv", "fhn"])
 def test_one_pass_equals_forward_and_backward(model, M, n_win):
@@ -192,3 +192,58 @@ def test_one_pass_equals_forward_and_backward(model, M, n_win):
         loss.backward()
         assert rel(s1, sde_r) < 2e-5
         assert rel(dz1, zr.grad) < 1e-4 and rel(dth1, thr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("M", [9, 258, 519, 2000])
+@pytest.mark.parametrize("model", ["lv", "sv"])
+def test_one_pass_plain_span(model, M):
+    """VissmElboData.plain_from (features.plain_from_table): windows whose mask / shift tables are dirty at element 0
+    (the reference's first window), in the middle of the chunk loop, at the last element, or nowhere.  The one-pass
+    kernel with the plain-span table equals the same kernel without it (the plain transform is the general one at
+    mask 1, shift 0) and the two-launch path's autograd."""
+    from viforssms_amd import _lib
+    from viforssms_amd.features import plain_from_table
+    from viforssms_amd.ops import ElboFeeds, elbo_terms, elbo_values_grad
+    B, n_win = 40, 5
+    d = _case(model, B, M, n_win, seed=M + len(model))
+    d["win"] = torch.arange(B, dtype=torch.int32) % n_win
+    D = 2 if model == "lv" else 1
+    mask, shift = d["mask"].reshape(n_win, D, M + 1), d["shift"].reshape(n_win, D, M + 1)
+    for w, pos in ((1, M // 2), (2, M), (3, min(4 * 65 + 1, M))):    # window 4: nowhere dirty
+        mask[w, D - 1, pos] = 0.5
+        shift[w, 0, max(pos - 1, 0)] = 1.5
+    pf = [int(plain_from_table(mask[w].numpy(), shift[w].numpy(), M)[0]) for w in range(n_win)]
+    assert pf[0] == 1 and pf[4] == 0 and pf[2] == M + 1
+    f = lambda k: d[k].float().to(DEV).contiguous() if k in d else None
+    kw = dict(obs=f("obs"), obs_bin=f("bin"), mask=f("mask"), shift=f("shift"), dim_one=f("dim_one"),
+              win=d["win"].to(DEV), n_win=n_win)
+    plain = ElboFeeds(**kw, plain_from=torch.tensor(pf, dtype=torch.int32, device=DEV))
+    general = ElboFeeds(**kw)
+    mid = {"lv": _lib.MODEL_LV, "sv": _lib.MODEL_SV}[model]
+    gs, go = f("gs"), (f("go") if model != "sv" else torch.zeros(B, device=DEV))
+    ge = f("ge") if model == "lv" else None
+    zd = d["z"].float().to(DEV).requires_grad_(True)
+    thd = d["theta"].float().to(DEV).requires_grad_(True)
+    sde, obs, ex = elbo_terms(mid, M, d["dt"], 1.0, general, zd, thd)
+    dl = (sde * gs).sum() + (obs * go).sum() + ((ex * ge).sum() if ge is not None else 0.0)
+    dl.backward()
+    a = elbo_values_grad(mid, M, d["dt"], 1.0, plain, zd.detach(), thd.detach(), gs, go, ge)
+    b = elbo_values_grad(mid, M, d["dt"], 1.0, general, zd.detach(), thd.detach(), gs, go, ge)
+    torch.cuda.synchronize()
+
+    def rel(x, y):
+        x, y = x.detach().double().cpu(), y.detach().double().cpu()
+        return float((x - y).norm() / (y.norm() + 1e-30))
+
+    for x, y in zip(a, b):
+        assert rel(x, y) < 1e-6
+    assert rel(a[0], sde) < 2e-6
+    assert rel(a[3], zd.grad) < 1e-6 and rel(a[4], thd.grad) < 1e-6
+    zr, thr = d["z"].clone().requires_grad_(True), d["theta"].clone().requires_grad_(True)
+    sde_r, obs_r, ex_r = _oracle(model, d, zr, thr)
+    loss = (sde_r * d["gs"]).sum() + ((obs_r * d["go"]).sum() if model != "sv" else 0.0)
+    if model == "lv":
+        loss = loss + (ex_r * d["ge"]).sum()
+    loss.backward()
+    assert rel(a[0], sde_r) < 2e-5
+    assert rel(a[3], zr.grad) < 1e-4 and rel(a[4], thr.grad) < 1e-4

@@ -9,6 +9,8 @@
 #include "common.hpp"
 #include "elbo_math.hpp"
 
+#include <type_traits>
+
 namespace vissm {
 namespace elbo {
 
@@ -122,8 +124,29 @@ struct Dev<VISSM_MODEL_LV> {
       *dil = g * *j;
     }
   }
-  template <int N>
+  // the transform where the window's mask is 1 and shift 0 (VissmElboData.plain_from): no mask / shift loads
+  __device__ static void tf_plain(float zz, float* x, float* j, float* il, float* dil) {
+    const float e = fexp(-::fabsf(zz));
+    const float L = flog1p01(e);
+    *x = ::fmaxf(zz, 0.f) + L;
+    const float r = frcp(1.f + e);
+    const float sg = zz >= 0.f ? r : e * r;  // sigmoid(z)
+    *j = sg;
+    *il = ::fmaxf(-zz, 0.f) + L;
+    *dil = sg - 1.f;
+  }
+  template <int N, bool PLAIN = false>
   __device__ void states(const float* zb, int t0, St (&o)[N]) const {
+    if constexpr (PLAIN) {
+      float zz[2 * N];
+      ldn<2 * N>(zb + 2 * t0, zz);
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        tf_plain(zz[2 * i], &o[i].x[0], &o[i].j[0], &o[i].il[0], &o[i].dil[0]);
+        tf_plain(zz[2 * i + 1], &o[i].x[1], &o[i].j[1], &o[i].il[1], &o[i].dil[1]);
+      }
+      return;
+    }
     float zz[2 * N], m0[N], m1[N], s0[N], s1[N];
     ldn<2 * N>(zb + 2 * t0, zz);
     ldn<N>(mk + t0, m0);
@@ -219,19 +242,21 @@ struct Dev<VISSM_MODEL_SV> {
     d1 = a.d.dim_one + static_cast<size_t>(w) * (M + 1);
     ob = bn = nullptr;
   }
-  template <int N>
+  template <int N, bool PLAIN = false>
   __device__ void states(const float* zb, int t0, St (&o)[N]) const {
     float zz[N], m[N], s[N], x1[N];
     ldn<N>(zb + t0, zz);
-    ldn<N>(mk + t0, m);
-    ldn<N>(sh + t0, s);
+    if constexpr (!PLAIN) {
+      ldn<N>(mk + t0, m);
+      ldn<N>(sh + t0, s);
+    }
     ldn<N>(d1 + t0, x1);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       o[i].x[0] = x1[i];
       o[i].j[0] = 0.f;
-      o[i].x[1] = zz[i] * m[i] + s[i];
-      o[i].j[1] = m[i];
+      o[i].x[1] = PLAIN ? zz[i] : zz[i] * m[i] + s[i];
+      o[i].j[1] = PLAIN ? 1.f : m[i];
     }
   }
   __device__ St state(const float* zb, int t) const {
@@ -297,7 +322,7 @@ struct Dev<VISSM_MODEL_FHN> {
     ob = a.d.obs + static_cast<size_t>(w) * 2 * M;
     bn = a.d.obs_bin + static_cast<size_t>(w) * 2 * M;
   }
-  template <int N>
+  template <int N, bool PLAIN = false>
   __device__ void states(const float* zb, int t0, St (&o)[N]) const {
     float zz[2 * N];
     ldn<2 * N>(zb + 2 * t0, zz);
@@ -703,13 +728,16 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     xc0 = s3.x[0];
     xc1 = s3.x[1];
   }
-  for (int c0 = 1; c0 < nfull; c0 += 64) {
+  // one iteration, specialised for a plain window span (no mask / shift) and for a full iteration (every lane owns
+  // a chunk: no masking of the sums)
+  auto iteration = [&](const int c0, auto plain_tag, auto full_tag) {
+    constexpr bool PLAIN = decltype(plain_tag)::value, FULL = decltype(full_tag)::value;
     const int c = c0 + lane;
-    const bool act = c < nfull;
+    const bool act = FULL || c < nfull;
     const float on = act ? 1.f : 0.f;
     const int t0 = kV * (act ? c : nfull - 1);   // idle lanes of the last iteration evaluate the last chunk, unused
     St st[kV];
-    m.template states<kV>(zb, t0, st);
+    m.template states<kV, PLAIN>(zb, t0, st);
     float y[2][kV], bb[2][kV];
     if constexpr (Dv::kObs) {  // rows t0 - 1 .. t0 + kV - 2 observe x_{t0} .. x_{t0+kV-1}
       ldn<kV>(m.ob + t0 - 1, y[0]);
@@ -731,7 +759,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
 #pragma unroll
     for (int j = 1; j < kV; ++j) tr[j] = m.trans(st[j - 1], st[j]);
 #pragma unroll
-    for (int j = 0; j < kV; ++j) count(tr[j], on);
+    for (int j = 0; j < kV; ++j) count(tr[j], FULL ? 1.f : on);
     // the head of the chunk's last element: lane l + 1's first transition
     const float hn0 = wave_shl1(tr[0].gh[0]), hn1 = wave_shl1(tr[0].gh[1]);
     // the previous iteration's deferred chunk: its head is this iteration's lane-0 first transition
@@ -762,7 +790,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
         g[0] += gs * tr[j + 1].gh[0];
         g[1] += gs * tr[j + 1].gh[1];
       }
-      obs_g(st[j], y[0][j], y[1][j], bb[0][j], bb[1][j], g, on);
+      obs_g(st[j], y[0][j], y[1][j], bb[0][j], bb[1][j], g, FULL ? 1.f : on);
       if (j + 1 == kV) {
         glast[0] = g[0];
         glast[1] = g[1];
@@ -771,7 +799,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
           g[1] += gs * hn1;
         }
       }
-      dz_of(st[j], g, true, on, o + ZD * j);
+      dz_of(st[j], g, true, FULL ? 1.f : on, o + ZD * j);
     }
     if (act && lane != dl) {
 #pragma unroll
@@ -797,6 +825,20 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     pt0 = kV * last_c;
     xc0 = lane_val(st[kV - 1].x[0], 63);
     xc1 = lane_val(st[kV - 1].x[1], 63);
+    };
+  const int pf = a.d.plain_from ? a.d.plain_from[w] : (1 << 30);   // first element of the plain span
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  for (int c0 = 1; c0 < nfull; c0 += 64) {
+    const bool plain = (MODEL != VISSM_MODEL_FHN) && kV * c0 >= pf;   // the whole iteration lies in the plain span
+    const bool full = c0 + 63 < nfull;
+    if (plain) {
+      if (full) iteration(c0, T_{}, T_{});
+      else iteration(c0, T_{}, F_{});
+    } else {
+      if (full) iteration(c0, F_{}, T_{});
+      else iteration(c0, F_{}, F_{});
+    }
   }
   // ---- element-wise tail: elements [0, kV) and [kV nfull, M] ----
   const int lo_end = nfull >= 1 ? kV : M + 1;

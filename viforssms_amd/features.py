@@ -133,6 +133,18 @@ def sv_table(obs, x0, T, dt, target_dims, n_flows, k, M, fw) -> FeatureTable:
                                                    "obs": np.asarray(obs, dtype=np.float64)})
 
 
+def plain_from_table(mask_vals, shift_vals, M: int) -> np.ndarray:
+    """VissmElboData.plain_from per window start s (int32): one past the last element of the window [s, s + M] whose
+    mask is not 1 or shift not 0 in any row, 0 when there is none -- from that element on the one-pass ELBO kernel
+    evaluates the transform without the mask / shift loads."""
+    mv, sv = np.atleast_2d(mask_vals), np.atleast_2d(shift_vals)
+    dirty = ((mv != 1.0) | (sv != 0.0)).any(0)
+    last = np.maximum.accumulate(np.where(dirty, np.arange(dirty.size), -1))   # last dirty position <= q
+    s = np.arange(max(dirty.size - M, 1))
+    ld = last[np.minimum(s + M, dirty.size - 1)]
+    return np.where(ld >= s, ld - s + 1, 0).astype(np.int32)
+
+
 class DeviceTable:
     """The FeatureTable's padded channel arrays (and the per-window feed tables) resident on the GPU,
     built once per model; ``batch(uniq_dev, n)`` gathers time_feats and the ELBO feeds of n window
@@ -156,6 +168,8 @@ class DeviceTable:
         if tab.family in ("lv", "sv"):
             self.extra["mask"] = f32(ex["mask_vals"])
             self.extra["shift"] = f32(ex["shift_vals"])
+            pf = plain_from_table(ex["mask_vals"], ex["shift_vals"], tab.M)
+            self.plain_from = torch.as_tensor(pf, device=device)
         if tab.family == "sv":
             self.extra["dim_one"] = f32(np.asarray(ex["obs"]).reshape(1, -1))
 
@@ -193,4 +207,6 @@ class DeviceTable:
             out = torch.empty(n, M + 1, dtype=torch.float32, device=dev)
             gather_windows(self.extra["dim_one"], uniq_dev, out, n, M + 1, 1, os=(M + 1, 1, 0))
             feeds["dim_one"] = out
+        if t.family in ("lv", "sv"):
+            feeds["plain_from"] = self.plain_from[uniq_dev.long()]
         return ts, feeds

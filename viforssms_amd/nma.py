@@ -453,7 +453,7 @@ class Engine:
         ts, f = self._dtab.batch(idx_dev[:n], n)
         win = idx_dev[n:] if n > 1 else None
         feeds = ElboFeeds(obs=f.get("obs"), obs_bin=f.get("obs_bin"), mask=f.get("mask"), shift=f.get("shift"),
-                          dim_one=f.get("dim_one"), win=win, n_win=n)
+                          dim_one=f.get("dim_one"), win=win, n_win=n, plain_from=f.get("plain_from"))
         return Batch(starts, uniq, ts, win, feeds, {})
 
     # ---- random inputs (Philox; keyed by global sample index so sharding is exact) ----

@@ -381,10 +381,11 @@ class ElboFeeds:
     dim_one: Optional[torch.Tensor] = None
     win: Optional[torch.Tensor] = None
     n_win: int = 1
+    plain_from: Optional[torch.Tensor] = None   # int32 [n_win]: VissmElboData.plain_from (None: NULL)
 
     def cdata(self) -> ElboData:
         return ElboData(ptr(self.win), ptr(self.obs), ptr(self.obs_bin), ptr(self.mask), ptr(self.shift),
-                        ptr(self.dim_one))
+                        ptr(self.dim_one), ptr(self.plain_from))
 
 
 class ElboFn(torch.autograd.Function):
