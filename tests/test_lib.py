@@ -60,6 +60,21 @@ def test_library_rejects_bad_shapes_without_gpu():
     assert rc < 0 and b"bad shape" in lib.vissm_last_error()
 
 
+def test_feature_kernels_refuse_kernel_shorter_than_stride():
+    """vissm_feat_*: a forward block writes s (kT - 1) + k rows and the backward reads s kT, so k < stride would leave
+    rows the backward reads unwritten; the shape check refuses it (host arithmetic only, no GPU)."""
+    from viforssms_amd import _lib
+    lib = _lib.load()
+
+    def ws(k, s, Lh=10):
+        d = _lib.FeatDesc(n_win=1, Lf=s * (Lh - 1) + k + 5, Cin=3, H=50, k=k, stride=s, Lh=Lh, in_win_stride=0)
+        return lib.vissm_feat_workspace_size(ctypes.byref(d))
+
+    assert ws(2, 2) > 0 and ws(1, 1) > 0 and ws(20, 2) > 0
+    assert ws(1, 2) == 0
+    assert b"kernel_len 1 < stride 2" in lib.vissm_last_error()
+
+
 def test_bf16x2_precisions_without_gpu():
     """VISSM_PREC_BF16X2 (split weights, bf16 activations) is a forward and backward precision with workspace on
     both sides; VISSM_PREC_BF16X2_BF16 belongs to the fused last AR flow only and the other entry points refuse it
