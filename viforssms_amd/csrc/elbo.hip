@@ -89,14 +89,12 @@ struct Dev<VISSM_MODEL_LV> {
   static constexpr int P = 3, ZD = 2, SU = 1;  // (registers: one chunk in flight per lane)
   static constexpr bool kObs = true, kExtra = true;
   static constexpr float kSd = 1.f;
-  float e0, e1, e2, dt, idt, c_lp;
+  float E0, E1, E2, c_lp;
   int M;
   const float *mk, *sh, *ob, *bn;  // window rows: mask / shift [2][M+1], obs / obs_bin [2][M]
   __device__ void init(const Args& a, const float* thp, int w) {
-    e0 = ::expf(thp[0]); e1 = ::expf(thp[1]); e2 = ::expf(thp[2]);
-    dt = a.dt;
-    idt = 1.f / dt;
-    c_lp = -::logf(dt) - em::kLog2Pi_;   // -1/2 log(dt^2) - log 2 pi
+    E0 = a.dt * ::expf(thp[0]); E1 = a.dt * ::expf(thp[1]); E2 = a.dt * ::expf(thp[2]);
+    c_lp = -em::kLog2Pi_;   // -1/2 log det Sigma is -1/2 log D: dt is inside the rates
     M = a.M;
     mk = a.d.mask + static_cast<size_t>(w) * 2 * (M + 1);
     sh = a.d.shift + static_cast<size_t>(w) * 2 * (M + 1);
@@ -116,7 +114,7 @@ struct Dev<VISSM_MODEL_LV> {
     const float sg = zz >= 0.f ? r : e * r;  // sigmoid(z)
     *j = m * sg;
     if (m == 1.f && s == 0.f) {
-      *il = ::fmaxf(-zz, 0.f) + L;
+      *il = L - ::fminf(zz, 0.f);   // max(-z, 0) + L: min(z, 0) shares max(z, 0)'s canonical z
       *dil = sg - 1.f;
     } else {
       float g;
@@ -132,7 +130,7 @@ struct Dev<VISSM_MODEL_LV> {
     const float r = frcp(1.f + e);
     const float sg = zz >= 0.f ? r : e * r;  // sigmoid(z)
     *j = sg;
-    *il = ::fmaxf(-zz, 0.f) + L;
+    *il = L - ::fminf(zz, 0.f);   // max(-z, 0) + L: min(z, 0) shares max(z, 0)'s canonical z
     *dil = sg - 1.f;
   }
   template <int N, bool PLAIN = false>
@@ -165,48 +163,36 @@ struct Dev<VISSM_MODEL_LV> {
     tf(zb[2 * t + 1], mk[M + 1 + t], sh[M + 1 + t], &o.x[1], &o.j[1], &o.il[1], &o.dil[1]);
     return o;
   }
-  // em::lv_trans with the exponentials hoisted, det / dt^2 = e0 x1 (Bv + e2 x2) + Bv e2 x2 (a sum of
-  // positive terms: no cancellation) and one reciprocal
+  // em::lv_trans with dt folded into the hoisted rates (E_i = dt e^{theta_i}): the rate terms a = E0 x1, b = E1 x1 x2,
+  // c = E2 x2 are the drift components (m = (a - b, b - c)) and the covariance entries (Sigma = [[a + b, -b],
+  // [-b, b + c]]) at once; det = a (b + c) + b c (a sum of positive terms: no cancellation), one reciprocal.
+  // Gradients through g = Sigma^-1 q: d lp / d Sigma_ij = (g_i g_j - Sigma^-1_ij) / 2, and each rate's theta
+  // gradient is (d lp / d rate) rate.
   __device__ em::TG trans(const St& p, const St& q) const {
     em::TG r;
     const float x1 = p.x[0], x2 = p.x[1];
-    const float p12 = x1 * x2;
-    const float Bv = e1 * p12, a1 = e0 * x1, c2 = e2 * x2;
-    const float A = a1 + Bv, Cc = Bv + c2;
-    const float m1 = dt * (a1 - Bv), m2 = dt * (Bv - c2);
-    const float q1 = q.x[0] - x1 - m1, q2 = q.x[1] - x2 - m2;
-    const float Dl = a1 * Cc + Bv * c2;
-    const float iD = frcp(Dl), inv = iD * idt;
-    const float g1 = inv * (Cc * q1 + Bv * q2), g2 = inv * (Bv * q1 + A * q2);
+    const float a = E0 * x1, e1x2 = E1 * x2, c = E2 * x2;
+    const float b = e1x2 * x1;
+    const float A = a + b, C = b + c;
+    const float q1 = q.x[0] - x1 - (a - b), q2 = q.x[1] - x2 - (b - c);
+    const float D = a * C + b * c;
+    const float iD = frcp(D);
+    const float g1 = iD * (C * q1 + b * q2), g2 = iD * (b * q1 + A * q2);
     const float quad = q1 * g1 + q2 * g2;
-    r.lp = -0.5f * flog(Dl) - 0.5f * quad + c_lp;
-    const float gq1 = -g1, gq2 = -g2;
-    float gA = -0.5f * Cc * iD - 0.5f * (q2 * q2 * inv - quad * Cc * iD);
-    float gC = -0.5f * A * iD - 0.5f * (q1 * q1 * inv - quad * A * iD);
-    float gB = Bv * iD - q1 * q2 * inv - quad * Bv * iD;
-    r.gt[0] = gq1;
-    r.gt[1] = gq2;
-    float gx1 = -gq1, gx2 = -gq2;
-    const float gm1 = -gq1, gm2 = -gq2;
-    float ge0 = gm1 * dt * x1, ge1 = 0.f, ge2 = -gm2 * dt * x2;
-    gx1 += gm1 * dt * e0;
-    gx2 += -gm2 * dt * e2;
-    gB += (gm2 - gm1) * dt;
-    gB += gC;
-    ge2 += gC * x2;
-    gx2 += gC * e2;
-    ge0 += gA * x1;
-    gx1 += gA * e0;
-    gB += gA;
-    ge1 += gB * p12;
-    const float gp = gB * e1;
-    gx1 += gp * x2;
-    gx2 += gp * x1;
-    r.gh[0] = gx1;
-    r.gh[1] = gx2;
-    r.gth[0] = ge0 * e0;
-    r.gth[1] = ge1 * e1;
-    r.gth[2] = ge2 * e2;
+    r.lp = -0.5f * flog(D) - 0.5f * quad + c_lp;
+    const float hD = 0.5f * iD;
+    const float gA = 0.5f * g1 * g1 - C * hD;        // d lp / d Sigma_11
+    const float gC = 0.5f * g2 * g2 - A * hD;        // d lp / d Sigma_22
+    const float gb = b * iD - g1 * g2;               // d lp / d b through the off-diagonal entries
+    const float Ga = gA + g1, Gc = gC - g2;          // + the drift: d lp / d m = g
+    const float Gb = gA + gC + gb - g1 + g2;
+    r.gt[0] = -g1;
+    r.gt[1] = -g2;
+    r.gh[0] = g1 + Ga * E0 + Gb * e1x2;
+    r.gh[1] = g2 + Gc * E2 + Gb * (E1 * x1);
+    r.gth[0] = Ga * a;
+    r.gth[1] = Gb * b;
+    r.gth[2] = Gc * c;
     r.gth[3] = r.gth[4] = 0.f;
     return r;
   }
