@@ -70,6 +70,9 @@ TRAJ = {  # precision -> (B, M, k, T, yardstick multiple, absolute floor, ELBO t
     "bf16": (20, 5000, 8, 5000, 0.0, 2e-5, 1e-4, 1e-4),
 }
 EMUL_SAFETY = 3.0
+if os.environ.get("VISSM_TRAJ_FP32_YARDSTICK"):   # diagnostics: also run the float32 oracle beside a reduced mode
+    for _m in ("bf16x2", "bf16x2f", "bf16"):
+        TRAJ[_m] = TRAJ[_m][:4] + (10.0,) + TRAJ[_m][5:]
 
 
 # the rounding models a mode's trajectory is held to: bf16x2f evaluates the ELBO with split weights but takes the
