@@ -54,6 +54,22 @@ int flow5_ar_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float
                    const float* theta_term, const float* theta, const float* obs, const float* obs_bin, float obs_std,
                    float scale, float* x, float* logsig, float* du, float* dC, float* dtheta_term,
                    const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st);
+// the same, built with the scheduler's register-pressure trackers (flow_v5f.hip): the fused flow's kernels run there
+// (VISSM_FUSED_TU=0: the flow_v5.hip build, A/B)
+bool flow5_ar_fused_supports_fz(const VissmFlowDesc* d);
+size_t flow5_ar_fused_workspace_size_fz(const VissmFlowDesc* d);
+int flow5_ar_fused_fz(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
+                      const int32_t* win, const float* theta_term, const float* theta, const float* obs,
+                      const float* obs_bin, float obs_std, float scale, float* x, float* logsig, float* du, float* dC,
+                      float* dtheta_term, const VissmFlowGrads* gr, void* workspace, size_t ws_bytes, hipStream_t st);
+#ifndef VISSM_FUSED_TU
+#define VISSM_FUSED_TU 1
+#endif
+#if VISSM_FUSED_TU
+#define FUSED_API(name) name##_fz
+#else
+#define FUSED_API(name) name
+#endif
 
 static bool use_flow4(const VissmFlowDesc* d) { return d->n_hidden <= 1; }
 
@@ -172,12 +188,12 @@ int32_t vissm_flow_kernel_precision(const VissmFlowDesc* d) {
 }
 
 int32_t vissm_flow_ar_elbo_fused_supported(const VissmFlowDesc* d) {
-  return (validate(d) == VISSM_OK && flow5_ar_fused_supports(d)) ? 1 : 0;
+  return (validate(d) == VISSM_OK && FUSED_API(flow5_ar_fused_supports)(d)) ? 1 : 0;
 }
 
 size_t vissm_flow_ar_elbo_fused_workspace_size(const VissmFlowDesc* d) {
   if (!vissm_flow_ar_elbo_fused_supported(d)) return 0;
-  return flow5_ar_fused_workspace_size(d);
+  return FUSED_API(flow5_ar_fused_workspace_size)(d);
 }
 
 int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C,
@@ -187,7 +203,7 @@ int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, c
                              size_t ws_bytes, void* stream) {
   int rc = validate(d);
   if (rc) return rc;
-  VISSM_CHECK_ARG(flow5_ar_fused_supports(d),
+  VISSM_CHECK_ARG(FUSED_API(flow5_ar_fused_supports)(d),
                   "flow_ar_elbo_fused: needs bf16 / bf16x3 (k <= 32) or bf16x2 / bf16x2_bf16 (k <= 8, one window), one hidden "
                   "layer, no BN, "
                   "stride 1");
@@ -198,8 +214,8 @@ int vissm_flow_ar_elbo_fused(const VissmFlowDesc* d, const VissmFlowParams* w, c
   VISSM_CHECK_ARG(obs_std > 0.f, "flow_ar_elbo_fused: obs_std must be positive");
   VISSM_CHECK_ARG(d->out_pitch == 0 || d->out_pitch == d->L - d->k, "flow_ar_elbo_fused: x is written dense (out_pitch "
                   "%d must be 0 or L - k)", d->out_pitch);
-  return flow5_ar_fused(d, w, u, C, win, theta_term, theta, obs, obs_bin, obs_std, scale, x, logsig, du, dC,
-                        dtheta_term, gr, workspace, ws_bytes, as_stream(stream));
+  return FUSED_API(flow5_ar_fused)(d, w, u, C, win, theta_term, theta, obs, obs_bin, obs_std, scale, x, logsig, du,
+                                   dC, dtheta_term, gr, workspace, ws_bytes, as_stream(stream));
 }
 
 }  // extern "C"
