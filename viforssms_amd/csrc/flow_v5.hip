@@ -1320,8 +1320,9 @@ __device__ __forceinline__ float swap_hi_lo(float v) {
 }
 constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 // Design decisions (A/B, AR-cfg launches):
-//  * compiler fences between the unit's phases in the fused (FZ) variant only (without them: middle flows 23.3 ->
-//    22.4 ms, the fused one 26.8 -> 28.2, the first flow unchanged);
+//  * compiler fences between the unit's phases in the fused (FZ) variant (without them: middle flows 23.3 ->
+//    22.4 ms, the fused one 26.8 -> 28.2, the first flow unchanged) and, since round 5, in the first flow's variant
+//    without du (18.31 -> 18.07 ms; the middle flows with them 20.57 -> 20.88: profiles/r05/ab_sched_strategies.log);
 //  * the recompute's ELU select as v_med3 (one instruction fewer per element): 93.3 -> 91.4 ms per AR-cfg step;
 //  * a t-chunk's look-back tile (fused variant) runs the whole unit with every gradient zero (nP = 0 masks them): a
 //    branch out after the recompute split the unit into basic blocks the scheduler cannot interleave across;
@@ -1337,6 +1338,9 @@ constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
 // Rejected: elu'(I_1) = min(2^x', 1) from the recompute's exp kept to the head backward (+1 ms per step: registers);
 // per-sample d theta for the whole item in a [h][16 samples] MFMA accumulator (16 more registers: 60 spilled);
 // s_setprio 1 for the second wave on each SIMD (-0.2 ms, noise).
+#ifndef VISSM_NODU_FENCES
+#define VISSM_NODU_FENCES 1   // (A/B switch: 0 leaves the first flow's variant without phase fences)
+#endif
 template <bool FZ>
 __device__ __forceinline__ void fence2() {
   if constexpr (FZ) fence();
@@ -1469,7 +1473,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       fz_bt = fz.bin[wo];
     }
     for (int bl = 0; bl < nb; bl += 2) {
-      fence2<FZ>();
+      fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
       const bool two = bl + 1 < nb;  // wave-uniform; else the second slot is a ghost
       const int blv[2] = {bl, two ? bl + 1 : bl};
       const int bv[2] = {b_lo + blv[0], b_lo + blv[1]};
@@ -1521,7 +1525,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       float mu[2], rr[2];
       {
         f4 acc[2][4];
-        fence2<FZ>();
+        fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
         Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c), u_frag<NP>(uwin[w][1], 1, 0, g, c)};
         if constexpr (TF) {
           if (g >= 2) {
@@ -1550,7 +1554,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
-        fence2<FZ>();
+        fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           if (g == 3) X[cb][3][3] = 1.f;  // the ones row: bias of the hidden layer
@@ -1582,7 +1586,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
-        fence2<FZ>();
+        fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -1702,7 +1706,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           }
         }
       }
-      fence2<FZ>();
+      fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
       // dW_head[h][o] += sum over both samples' positions of I_1[h][p] G[o][p] (K = 32): block 3 of the same
       // fragments is the B operand (its columns 5, 6 are the G rows)
       {
@@ -1733,7 +1737,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             D[cb][rb] = mfma16(wa, gf2, d0);
           }
         }
-        fence2<FZ>();
+        fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
@@ -1744,7 +1748,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
         }
       }
-      fence2<FZ>();
+      fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
       // dX = W~ dZ (chain), both samples
       f4 dX[2][4];
 #pragma unroll
@@ -1764,7 +1768,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
           }
         }
       }
-      fence2<FZ>();
+      fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
       // dW += I_0 dZ^T over both samples' positions (K = 32), from the two images
       {
         bf8 dzf[4];
@@ -1822,7 +1826,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
             for (int r = 0; r < 4; ++r) dscr[w][cb][4 * g + r][c + 4 * g + r] = dcn[cb][r];
         }
       }
-      fence2<FZ>();
+      fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
       // dW_eps and d theta from dA0's position-contracted fragments (K = 32)
       {
         const unsigned one2 = 0x3F803F80u;
@@ -1869,7 +1873,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       // du over local positions q in [0, nP + k) for both samples at once: lane = 32 cb + q
       if constexpr (DU) {
-        fence2<FZ>();
+        fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
         const int cbq = lane >> 5, q = lane & 31;
         const int lim = nP + a.k;
         const bool act = q < lim && (cbq == 0 || two);
