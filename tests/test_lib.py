@@ -75,6 +75,23 @@ def test_feature_kernels_refuse_kernel_shorter_than_stride():
     assert b"kernel_len 1 < stride 2" in lib.vissm_last_error()
 
 
+def test_elbo_fwd_grad_checks_without_gpu():
+    """vissm_elbo_fwd_grad (the training step's one-pass log-density call): a null z / dz is refused and B = 0 is a
+    no-op, before any device work; VissmElboData carries plain_from as its last field (include/vissm.h)."""
+    from viforssms_amd import _lib
+    lib = _lib.load()
+    assert [f[0] for f in _lib.ElboData._fields_][-1] == "plain_from"
+    fake = ctypes.c_void_p(16)   # never dereferenced: the checks run first
+    d = _lib.ElboDesc(_lib.MODEL_FHN, 4, 10, 1, 0.1, 1.0)
+    data = _lib.ElboData(None, fake, fake, None, None, None, None)
+    rc = lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(data), None, fake, fake, fake, None, fake, fake,
+                                 None, fake, fake, None)
+    assert rc < 0 and b"null pointer" in lib.vissm_last_error()
+    d0 = _lib.ElboDesc(_lib.MODEL_FHN, 0, 10, 1, 0.1, 1.0)
+    assert lib.vissm_elbo_fwd_grad(ctypes.byref(d0), ctypes.byref(data), fake, fake, fake, fake, None, fake, fake,
+                                   None, fake, fake, None) == 0
+
+
 def test_bf16x2_precisions_without_gpu():
     """VISSM_PREC_BF16X2 (split weights, bf16 activations) is a forward and backward precision with workspace on
     both sides; VISSM_PREC_BF16X2_BF16 belongs to the fused last AR flow only and the other entry points refuse it
