@@ -396,6 +396,17 @@ int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, 
                     const float* dtheta, const float* dlogq, float* dw, void* workspace,
                     size_t ws_bytes, void* stream);
 
+/* The flows' theta branch backward (IAF._create_flow's three linear dense layers on theta, AR.py:63-68;
+ * lotka_volterra_partial.py:84-89): theta_term = ((theta W0 + b0) W1 + b1) W2 + b2 with W0 [P][n0], W1 [n0][n1],
+ * W2 [n1][H]; given dterm = d loss / d theta_term [B][H] it writes dtheta [B][P] and the six weight gradients
+ * (overwritten, not accumulated).  P <= 8, n0 / n1 / H <= 64; deterministic (fixed-order sums); workspace from
+ * vissm_theta_branch_bwd_workspace_size(B, P) (0: bad shape). */
+size_t vissm_theta_branch_bwd_workspace_size(int32_t B, int32_t P);
+int vissm_theta_branch_bwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t H, const float* theta,
+                           const float* dterm, const float* W0, const float* b0, const float* W1, const float* b1,
+                           const float* W2, float* dtheta, float* dW0, float* db0, float* dW1, float* db1,
+                           float* dW2, float* db2, void* workspace, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Opt-in kernel timing (for bench.py's live roofline): when enabled, the flow
  * entry points bracket their main kernel with hipEvents on the launch stream.

@@ -100,3 +100,28 @@ def test_theta_backward_deterministic_and_accumulates():
         ((th * gth).sum() + (lq * glq).sum()).backward()
     torch.cuda.synchronize()
     assert torch.allclose(st.grad, 2 * g1, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,P", [(1, 3), (63, 3), (64, 3), (65, 4), (1000, 3), (65536, 3), (4097, 8)])
+def test_theta_branch_backward_kernel(B, P):
+    """vissm_theta_branch_bwd (the flows' theta branch, nma._ThetaBranch: ((theta W0 + b0) W1 + b1) W2 + b2,
+    AR.py:63-68) against float64 autograd of the three layers, every output to fp32 summation order, and bitwise
+    reproducible."""
+    from viforssms_amd.ops import theta_branch_bwd
+    g = torch.Generator().manual_seed(B + P)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
+    H = 50
+    theta, d = r(B, P), r(B, H)
+    W0, b0, W1, b1, W2, b2 = r(P, 50) * 0.3, r(50) * 0.1, r(50, 50) * 0.14, r(50) * 0.1, r(50, H) * 0.14, r(H) * 0.1
+    leaves = [t.clone().requires_grad_(True) for t in (theta, W0, b0, W1, b1, W2, b2)]
+    th, w0, c0, w1, c1, w2, c2 = leaves
+    (((th @ w0 + c0) @ w1 + c1) @ w2 + c2).backward(d)
+    ref = [t.grad for t in leaves]
+    dev = lambda t: t.float().cuda()
+    got = theta_branch_bwd(*(dev(t) for t in (theta, d, W0, b0, W1, b1, W2)))
+    again = theta_branch_bwd(*(dev(t) for t in (theta, d, W0, b0, W1, b1, W2)))
+    torch.cuda.synchronize()
+    for name, a, b, c in zip(("dtheta", "dW0", "db0", "dW1", "db1", "dW2", "db2"), got, again, ref):
+        assert torch.equal(a, b), name
+        err = float((a.double().cpu() - c).norm() / (c.norm() + 1e-30))
+        assert err < 1e-5, (name, err)

@@ -367,4 +367,243 @@ int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, 
   return VISSM_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// The flows' theta branch (IAF._create_flow's three linear dense layers on theta, AR.py:63-68):
+// theta_term = ((theta W0 + b0) W1 + b1) W2 + b2, with d = d loss / d theta_term [B, H].  Every gradient follows
+// from S = theta^T d [P, H], s = sum_b d [H] and dtheta = d (W0 W1 W2)^T [B, P] (nma._ThetaBranch): one pass over d
+// (one wave per 32-row slice, lane = column h: S / s partials per block, dtheta rows by wave reductions; each block
+// forms W0 W1 W2 from the LDS-staged weights), then one block sums the partials in a fixed order and forms the
+// [<= 64]^2 weight gradients.  Two launches instead of the ~14 small library kernels of the torch form.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+namespace vissm {
+namespace {
+constexpr int kTbMax = 64;   // H, n0, n1 <= 64, P <= 8
+constexpr int kTbRows = 32;  // rows of d per wave
+
+// the three weight matrices staged in LDS (W0 [P][n0], W1 [n0][n1], W2 [n1][H], row pitch kTbMax)
+struct TbW {
+  float W0[8][kTbMax], W1[kTbMax][kTbMax], W2[kTbMax][kTbMax];
+};
+__device__ void tb_stage(TbW& w, int P, int n0, int n1, int H, const float* __restrict__ W0,
+                         const float* __restrict__ W1, const float* __restrict__ W2) {
+  for (int i = threadIdx.x; i < P * n0; i += blockDim.x) w.W0[i / n0][i % n0] = W0[i];
+  for (int i = threadIdx.x; i < n0 * n1; i += blockDim.x) w.W1[i / n1][i % n1] = W1[i];
+  for (int i = threadIdx.x; i < n1 * H; i += blockDim.x) w.W2[i / H][i % H] = W2[i];
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void theta_branch_pass_kernel(int B, int n0, int n1, int H,
+                                                                 const float* __restrict__ theta,
+                                                                 const float* __restrict__ d,
+                                                                 const float* __restrict__ W0g,
+                                                                 const float* __restrict__ W1g,
+                                                                 const float* __restrict__ W2g,
+                                                                 float* __restrict__ dtheta, float* __restrict__ part) {
+  // Wc = W0 W1 W2 [P][H], formed by every block from the LDS-staged weights (no separate launch)
+  __shared__ TbW w;
+  __shared__ float W01[P][kTbMax], Wc[P][kTbMax];
+  tb_stage(w, P, n0, n1, H, W0g, W1g, W2g);
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * n1; i += 256) {
+    const int p = i / n1, jj = i % n1;
+    float v = 0.f;
+    for (int a = 0; a < n0; ++a) v += w.W0[p][a] * w.W1[a][jj];
+    W01[p][jj] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * H; i += 256) {
+    const int p = i / H, h = i % H;
+    float v = 0.f;
+    for (int jj = 0; jj < n1; ++jj) v += W01[p][jj] * w.W2[jj][h];
+    Wc[p][h] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r0 = wv * kTbRows;
+  const bool on = lane < H;
+  float wc[P], sacc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    wc[p] = on ? Wc[p][lane] : 0.f;
+    sacc[p] = 0.f;
+  }
+  float ssum = 0.f;
+  const int r1 = min(B, r0 + kTbRows);
+  constexpr int RB = 8;   // rows whose loads are in flight together
+  for (int rb = r0; rb < r1; rb += RB) {
+    float v[RB], t[RB][P];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = min(rb + i, r1 - 1);   // (rows past r1 are loaded again and not counted)
+      v[i] = on ? d[static_cast<size_t>(r) * H + lane] : 0.f;
+#pragma unroll
+      for (int p = 0; p < P; ++p) t[i][p] = theta[static_cast<size_t>(r) * P + p];
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      if (rb + i >= r1) break;   // wave-uniform
+      float q[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        sacc[p] += t[i][p] * v[i];
+        q[p] = v[i] * wc[p];
+      }
+      ssum += v[i];
+      // dtheta[r][p] = sum_h d[r][h] Wc[p][h]: a fixed-order butterfly over the wave
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] += __shfl_xor(q[p], off);
+      if (lane < P) {
+        float o = q[0];
+#pragma unroll
+        for (int p = 1; p < P; ++p) o = lane == p ? q[p] : o;
+        dtheta[static_cast<size_t>(rb + i) * P + lane] = o;
+      }
+    }
+  }
+  // the block's partials (rows p = 0..P-1 of S, row P of s): the four waves' sums in wave order
+  __shared__ float wsum[4][P + 1][kTbMax];
+  const int wq = threadIdx.x >> 6;
+#pragma unroll
+  for (int p = 0; p < P; ++p) wsum[wq][p][lane] = sacc[p];
+  wsum[wq][P][lane] = ssum;
+  __syncthreads();
+  float* pb = part + static_cast<size_t>(blockIdx.x) * (P + 1) * kTbMax;
+  for (int i = threadIdx.x; i < (P + 1) * kTbMax; i += 256) {
+    const int p = i / kTbMax, h = i % kTbMax;
+    pb[i] = ((wsum[0][p][h] + wsum[1][p][h]) + wsum[2][p][h]) + wsum[3][p][h];
+  }
+}
+
+// S, s from the block partials in a fixed order, then the weight gradients (one block of 1024 threads)
+__global__ __launch_bounds__(1024) void theta_branch_finish_kernel(int n_rows, int P, int n0, int n1, int H,
+                                                                    const float* __restrict__ part,
+                                                                    const float* __restrict__ W0g,
+                                                                    const float* __restrict__ b0,
+                                                                    const float* __restrict__ W1g,
+                                                                    const float* __restrict__ b1,
+                                                                    const float* __restrict__ W2g,
+                                                                    float* __restrict__ dW0, float* __restrict__ db0,
+                                                                    float* __restrict__ dW1, float* __restrict__ db1,
+                                                                    float* __restrict__ dW2, float* __restrict__ db2) {
+  __shared__ TbW w;
+  __shared__ float S[9][kTbMax];      // rows 0..P-1: S, row P: s
+  __shared__ float SW2[9][kTbMax];    // rows 0..P-1: S W2^T, row P: s W2^T
+  __shared__ float W01[8][kTbMax], c1[kTbMax];
+  constexpr int NS = 8;               // row slices summed in parallel
+  __shared__ float sl[NS][9 * kTbMax];
+  const int R = P + 1;
+  tb_stage(w, P, n0, n1, H, W0g, W1g, W2g);
+  // thread (slice q, column i) sums rows q, q + NS, ... in order (eight loads in flight), then the slices are added
+  // in slice order: a fixed order for a given n_rows
+  for (int jx = threadIdx.x; jx < NS * R * kTbMax; jx += blockDim.x) {
+    const int q = jx / (R * kTbMax), i = jx % (R * kTbMax);
+    float v = 0.f;
+    int r = q;
+    for (; r + 7 * NS < n_rows; r += 8 * NS) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = part[static_cast<size_t>(r + NS * u) * R * kTbMax + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; r < n_rows; r += NS) v += part[static_cast<size_t>(r) * R * kTbMax + i];
+    sl[q][i] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < R * kTbMax; i += blockDim.x) {
+    float v = sl[0][i];
+#pragma unroll
+    for (int q = 1; q < NS; ++q) v += sl[q][i];
+    S[i / kTbMax][i % kTbMax] = v;
+  }
+  for (int i = threadIdx.x; i < P * n1; i += blockDim.x) {    // W0 W1
+    const int p = i / n1, j = i % n1;
+    float v = 0.f;
+    for (int a = 0; a < n0; ++a) v += w.W0[p][a] * w.W1[a][j];
+    W01[p][j] = v;
+  }
+  for (int j = threadIdx.x; j < n1; j += blockDim.x) {        // b0 W1 + b1
+    float v = b1[j];
+    for (int a = 0; a < n0; ++a) v += b0[a] * w.W1[a][j];
+    c1[j] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < R * n1; i += blockDim.x) {    // [S; s] W2^T
+    const int p = i / n1, j = i % n1;
+    float v = 0.f;
+    for (int h = 0; h < H; ++h) v += S[p][h] * w.W2[j][h];
+    SW2[p][j] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n1 * H; i += blockDim.x) {    // dW2 = (W0 W1)^T S + (b0 W1 + b1) s^T
+    const int j = i / H, h = i % H;
+    float v = c1[j] * S[P][h];
+    for (int p = 0; p < P; ++p) v += W01[p][j] * S[p][h];
+    dW2[i] = v;
+  }
+  for (int h = threadIdx.x; h < H; h += blockDim.x) db2[h] = S[P][h];
+  for (int j = threadIdx.x; j < n1; j += blockDim.x) db1[j] = SW2[P][j];
+  for (int i = threadIdx.x; i < n0 * n1; i += blockDim.x) {   // dW1 = W0^T (S W2^T) + b0 (s W2^T)^T
+    const int a = i / n1, j = i % n1;
+    float v = b0[a] * SW2[P][j];
+    for (int p = 0; p < P; ++p) v += w.W0[p][a] * SW2[p][j];
+    dW1[i] = v;
+  }
+  for (int i = threadIdx.x; i < R * n0; i += blockDim.x) {    // dW0 = (S W2^T) W1^T, db0 = (s W2^T) W1^T
+    const int p = i / n0, a = i % n0;
+    float v = 0.f;
+    for (int j = 0; j < n1; ++j) v += SW2[p][j] * w.W1[a][j];
+    if (p < P) dW0[i] = v;
+    else db0[a] = v;
+  }
+}
+}  // namespace
+}  // namespace vissm
+
+extern "C" {
+using namespace vissm;
+
+size_t vissm_theta_branch_bwd_workspace_size(int32_t B, int32_t P) {
+  if (B < 1 || P < 1 || P > 8) return 0;
+  const size_t waves = (static_cast<size_t>(B) + kTbRows - 1) / kTbRows;
+  return align_up(((waves + 3) / 4) * (P + 1) * kTbMax * sizeof(float));
+}
+
+int vissm_theta_branch_bwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t H, const float* theta,
+                           const float* dterm, const float* W0, const float* b0, const float* W1, const float* b1,
+                           const float* W2, float* dtheta, float* dW0, float* db0, float* dW1, float* db1,
+                           float* dW2, float* db2, void* workspace, size_t ws_bytes, void* stream) {
+  VISSM_CHECK_ARG(B >= 1 && P >= 1 && P <= 8 && n0 >= 1 && n0 <= kTbMax && n1 >= 1 && n1 <= kTbMax && H >= 1 &&
+                      H <= kTbMax,
+                  "theta_branch_bwd: bad shape (B >= 1, P <= 8, n0 / n1 / H <= %d)", kTbMax);
+  VISSM_CHECK_ARG(theta && dterm && W0 && b0 && W1 && b1 && W2 && dtheta && dW0 && db0 && dW1 && db1 && dW2 && db2,
+                  "theta_branch_bwd: null pointer");
+  VISSM_CHECK_ARG(workspace && ws_bytes >= vissm_theta_branch_bwd_workspace_size(B, P),
+                  "theta_branch_bwd: workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  const int waves = (B + kTbRows - 1) / kTbRows;
+  const int blocks = (waves + 3) / 4;
+  switch (P) {
+#define TB_CASE(PP)                                                                                             \
+  case PP:                                                                                                      \
+    hipLaunchKernelGGL(theta_branch_pass_kernel<PP>, dim3(blocks), dim3(256), 0, st, B, n0, n1, H, theta, dterm, \
+                       W0, W1, W2, dtheta, part);                                                              \
+    break;
+    TB_CASE(1) TB_CASE(2) TB_CASE(3) TB_CASE(4) TB_CASE(5) TB_CASE(6) TB_CASE(7) TB_CASE(8)
+#undef TB_CASE
+  }
+  VISSM_CHECK_LAUNCH("theta_branch_pass");
+  // (waves past ceil(B / kTbRows) in the last block add zero partials)
+  hipLaunchKernelGGL(theta_branch_finish_kernel, dim3(1), dim3(1024), 0, st, blocks, P, n0, n1, H, part, W0, b0,
+                     W1, b1, W2, dW0, db0, dW1, db1, dW2, db2);
+  VISSM_CHECK_LAUNCH("theta_branch_finish");
+  return VISSM_OK;
+}
+
 }  // extern "C"

@@ -26,7 +26,7 @@ import torch
 from . import _lib
 from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
                   ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad,
-                  elbo_values_grad)
+                  elbo_values_grad, theta_branch_bwd)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, linear_bf16, linear_x3, tn_split_k
@@ -54,6 +54,11 @@ class _ThetaBranch(torch.autograd.Function):
     def backward(ctx, d):
         theta, W0, b0, W1, b1, W2, W12 = ctx.saved_tensors
         d = d.contiguous()
+        if (d.is_cuda and theta.shape[1] <= 8 and max(W0.shape[1], W1.shape[1], W2.shape[1]) <= 64
+                and os.environ.get("VISSM_THETA_BRANCH_TORCH") != "1"):
+            # one pass over d for S, s and dtheta, then the [<= 64]^2 algebra in one block (vissm_theta_branch_bwd:
+            # three launches for the ~14 small library kernels below)
+            return theta_branch_bwd(theta, d, W0, b0, W1, b1, W2)
         S = tn_split_k(theta.contiguous(), d)      # theta^T d      [P, H]
         s = d.sum(0)                                # sum_b d        [H]
         SW2, sW2 = S @ W2.t(), s @ W2.t()           # through layer 2: theta^T dh1, sum dh1

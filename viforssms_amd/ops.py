@@ -95,6 +95,23 @@ def _dense_layout(t: torch.Tensor) -> bool:
     return True
 
 
+def theta_branch_bwd(theta, d, W0, b0, W1, b1, W2):
+    """The flows' theta-branch backward (include/vissm.h vissm_theta_branch_bwd; nma._ThetaBranch): dtheta and the
+    gradients of (W0, b0, W1, b1, W2, b2) from d = d loss / d theta_term, in three launches."""
+    lib = _lib.load()
+    _require_gpu(theta, d, W0, b0, W1, b1, W2)
+    B, P = theta.shape
+    n0, n1, H = W0.shape[1], W1.shape[1], W2.shape[1]
+    dev = d.device
+    args = [t.contiguous().float() for t in (theta, d, W0, b0, W1, b1, W2)]
+    outs = [torch.empty(sh, device=dev) for sh in ((B, P), (P, n0), (n0,), (n0, n1), (n1,), (n1, H), (H,))]
+    nb = lib.vissm_theta_branch_bwd_workspace_size(B, P)
+    ws = _workspace(nb, dev)
+    check(lib.vissm_theta_branch_bwd(B, P, n0, n1, H, *[ptr(t) for t in args], *[ptr(t) for t in outs], ptr(ws), nb,
+                                     _lib.stream_handle(dev)), "vissm_theta_branch_bwd")
+    return tuple(outs)
+
+
 def split_bf16(x: torch.Tensor):
     """(hi, lo) bf16 planes with x = hi + lo to ~2^-16 relative (vissm_split_bf16, one pass over x), laid out with
     x's strides: x may be a transposed view (LV's time-mixing features)."""
