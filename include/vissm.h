@@ -401,6 +401,12 @@ int vissm_theta_bwd(const VissmThetaDesc* d, const float* w, const float* mask, 
  * W2 [n1][H]; given dterm = d loss / d theta_term [B][H] it writes dtheta [B][P] and the six weight gradients
  * (overwritten, not accumulated).  P <= 8, n0 / n1 / H <= 64; deterministic (fixed-order sums); workspace from
  * vissm_theta_branch_bwd_workspace_size(B, P) (0: bad shape). */
+/* its forward: the collapsed weights Wc = W0 W1 W2 [P][H], bc = (b0 W1 + b1) W2 + b2 [H] (the factors the AR flow
+ * kernels fold into their layer-0 product, VissmFlowParams.theta_rank) and, when theta_term is not NULL,
+ * theta_term = theta Wc + bc [B][H]. */
+int vissm_theta_branch_fwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t H, const float* theta,
+                           const float* W0, const float* b0, const float* W1, const float* b1, const float* W2,
+                           const float* b2, float* Wc, float* bc, float* theta_term, void* stream);
 size_t vissm_theta_branch_bwd_workspace_size(int32_t B, int32_t P);
 int vissm_theta_branch_bwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t H, const float* theta,
                            const float* dterm, const float* W0, const float* b0, const float* W1, const float* b1,

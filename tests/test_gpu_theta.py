@@ -125,3 +125,24 @@ def test_theta_branch_backward_kernel(B, P):
         assert torch.equal(a, b), name
         err = float((a.double().cpu() - c).norm() / (c.norm() + 1e-30))
         assert err < 1e-5, (name, err)
+
+
+@pytest.mark.parametrize("B,P", [(0, 3), (1, 3), (1000, 3), (65536, 3), (77, 8)])
+def test_theta_branch_forward_kernel(B, P):
+    """vissm_theta_branch_fwd: the collapsed weights Wc = W0 W1 W2, bc = (b0 W1 + b1) W2 + b2 and theta_term =
+    theta Wc + bc against float64 (AR.py:63-68's three dense layers), and the GPU IAF path's theta_term / theta
+    gradient against the torch form of the same module (VISSM_THETA_BRANCH_TORCH=1)."""
+    from viforssms_amd.ops import theta_branch_fwd
+    g = torch.Generator().manual_seed(B + 7 * P)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
+    theta = r(B, P)
+    W0, b0, W1, b1, W2, b2 = r(P, 50) * 0.3, r(50) * 0.1, r(50, 50) * 0.14, r(50) * 0.1, r(50, 50) * 0.14, r(50) * 0.1
+    ref = ((theta @ W0 + b0) @ W1 + b1) @ W2 + b2
+    Wc_ref, bc_ref = W0 @ W1 @ W2, (b0 @ W1 + b1) @ W2 + b2
+    tt, Wc, bc = theta_branch_fwd(*(t.float().cuda() for t in (theta, W0, b0, W1, b1, W2, b2)))
+    torch.cuda.synchronize()
+    rel = lambda a, b: float((a.double().cpu() - b).norm() / (b.norm() + 1e-30))
+    assert rel(Wc, Wc_ref) < 1e-6 and rel(bc, bc_ref) < 1e-6
+    assert tt.shape == (B, 50)
+    if B:
+        assert rel(tt, ref) < 1e-6

@@ -135,6 +135,7 @@ SIGNATURES = {
     "vissm_theta_workspace_size": (_size_t, [ctypes.POINTER(ThetaDesc)]),
     "vissm_theta_fwd": (_i32, [ctypes.POINTER(ThetaDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                _c_void_p]),
+    "vissm_theta_branch_fwd": (_i32, [_i32] * 5 + [_c_void_p] * 10 + [_c_void_p]),
     "vissm_theta_branch_bwd_workspace_size": (_size_t, [_i32, _i32]),
     "vissm_theta_branch_bwd": (_i32, [_i32] * 5 + [_c_void_p] * 15 + [_size_t, _c_void_p]),
     "vissm_theta_bwd": (_i32, [ctypes.POINTER(ThetaDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

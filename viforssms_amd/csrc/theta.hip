@@ -562,6 +562,47 @@ __global__ __launch_bounds__(1024) void theta_branch_finish_kernel(int n_rows, i
     else db0[a] = v;
   }
 }
+// the collapsed theta-branch weights (one block): Wc = W0 W1 W2 [P][H], bc = (b0 W1 + b1) W2 + b2 [H]
+__global__ __launch_bounds__(256) void theta_branch_fold_kernel(int P, int n0, int n1, int H,
+                                                                 const float* __restrict__ W0g,
+                                                                 const float* __restrict__ b0,
+                                                                 const float* __restrict__ W1g,
+                                                                 const float* __restrict__ b1,
+                                                                 const float* __restrict__ W2g,
+                                                                 const float* __restrict__ b2, float* __restrict__ Wc,
+                                                                 float* __restrict__ bc) {
+  __shared__ TbW w;
+  __shared__ float W01[9][kTbMax];   // rows 0..P-1: W0 W1, row P: b0 W1 + b1
+  tb_stage(w, P, n0, n1, H, W0g, W1g, W2g);
+  __syncthreads();
+  for (int i = threadIdx.x; i < (P + 1) * n1; i += 256) {
+    const int p = i / n1, j = i % n1;
+    float v = p < P ? 0.f : b1[j];
+    for (int a = 0; a < n0; ++a) v += (p < P ? w.W0[p][a] : b0[a]) * w.W1[a][j];
+    W01[p][j] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (P + 1) * H; i += 256) {
+    const int p = i / H, h = i % H;
+    float v = p < P ? 0.f : b2[h];
+    for (int j = 0; j < n1; ++j) v += W01[p][j] * w.W2[j][h];
+    if (p < P) Wc[p * H + h] = v;
+    else bc[h] = v;
+  }
+}
+
+// theta_term[b][h] = theta[b] Wc[:, h] + bc[h] (one thread per output)
+__global__ __launch_bounds__(256) void theta_branch_term_kernel(int B, int P, int H, const float* __restrict__ theta,
+                                                                 const float* __restrict__ Wc,
+                                                                 const float* __restrict__ bc,
+                                                                 float* __restrict__ out) {
+  const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= static_cast<size_t>(B) * H) return;
+  const int b = static_cast<int>(i / H), h = static_cast<int>(i % H);
+  float v = bc[h];
+  for (int p = 0; p < P; ++p) v += theta[static_cast<size_t>(b) * P + p] * Wc[p * H + h];
+  out[i] = v;
+}
 }  // namespace
 }  // namespace vissm
 
@@ -603,6 +644,28 @@ int vissm_theta_branch_bwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t
   hipLaunchKernelGGL(theta_branch_finish_kernel, dim3(1), dim3(1024), 0, st, blocks, P, n0, n1, H, part, W0, b0,
                      W1, b1, W2, dW0, db0, dW1, db1, dW2, db2);
   VISSM_CHECK_LAUNCH("theta_branch_finish");
+  return VISSM_OK;
+}
+
+
+int vissm_theta_branch_fwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t H, const float* theta,
+                           const float* W0, const float* b0, const float* W1, const float* b1, const float* W2,
+                           const float* b2, float* Wc, float* bc, float* theta_term, void* stream) {
+  VISSM_CHECK_ARG(B >= 0 && P >= 1 && P <= 8 && n0 >= 1 && n0 <= kTbMax && n1 >= 1 && n1 <= kTbMax && H >= 1 &&
+                      H <= kTbMax,
+                  "theta_branch_fwd: bad shape (B >= 0, P <= 8, n0 / n1 / H <= %d)", kTbMax);
+  VISSM_CHECK_ARG(W0 && b0 && W1 && b1 && W2 && b2 && Wc && bc && (B == 0 || !theta_term || theta),
+                  "theta_branch_fwd: null pointer");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(theta_branch_fold_kernel, dim3(1), dim3(256), 0, st, P, n0, n1, H, W0, b0, W1, b1, W2, b2, Wc,
+                     bc);
+  VISSM_CHECK_LAUNCH("theta_branch_fold");
+  if (theta_term && B > 0) {
+    const size_t n = static_cast<size_t>(B) * H;
+    hipLaunchKernelGGL(theta_branch_term_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st, B, P,
+                       H, theta, Wc, bc, theta_term);
+    VISSM_CHECK_LAUNCH("theta_branch_term");
+  }
   return VISSM_OK;
 }
 

@@ -26,7 +26,7 @@ import torch
 from . import _lib
 from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
                   ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad,
-                  elbo_values_grad, theta_branch_bwd)
+                  elbo_values_grad, theta_branch_bwd, theta_branch_fwd)
 from .params import ParamStore, glorot_uniform
 from .theta_flow import ThetaFlow
 from .linalg import linear, linear_bf16, linear_x3, tn_split_k
@@ -67,6 +67,24 @@ class _ThetaBranch(torch.autograd.Function):
         dW0 = SW2 @ W1.t()                                      # theta^T dh0, dh0 = dh1 W1^T
         dtheta = d @ (W0 @ W12).t()
         return dtheta, dW0, sW2 @ W1.t(), dW1, sW2, dW2, s
+
+
+class _ThetaBranchK(torch.autograd.Function):
+    """_ThetaBranch on the GPU in two launches each way (vissm_theta_branch_fwd / _bwd): returns theta_term and the
+    collapsed weights (Wc, bc) it was formed with, which the two-sample AR kernels' theta fold takes as constants
+    (IAF.theta_factors reuses them: no second evaluation)."""
+
+    @staticmethod
+    def forward(ctx, theta, W0, b0, W1, b1, W2, b2):
+        ctx.save_for_backward(theta, W0, b0, W1, b1, W2)
+        tt, Wc, bc = theta_branch_fwd(theta, W0, b0, W1, b1, W2, b2)
+        ctx.mark_non_differentiable(Wc, bc)
+        return tt, Wc, bc
+
+    @staticmethod
+    def backward(ctx, d, _dWc, _dbc):
+        theta, W0, b0, W1, b1, W2 = ctx.saved_tensors
+        return theta_branch_bwd(theta, d.contiguous(), W0, b0, W1, b1, W2)
 
 
 class _SumGradOverRanks(torch.autograd.Function):
@@ -250,6 +268,9 @@ class IAF:
         forms (the same fp32 products), passed to the flow kernels as constants (VissmFlowParams.theta_rank) so
         the two-sample AR kernels form the theta term inside their layer-0 product; the gradient still flows
         through theta_term."""
+        st = getattr(self, "_fold", None)
+        if st is not None and st[0] is theta:   # the collapsed weights theta_term was just formed with
+            return theta.detach().contiguous(), st[1], st[2]
         p = self._p
         with torch.no_grad():
             W1, W2 = p("theta1/kernel"), p("theta2/kernel")
@@ -259,8 +280,15 @@ class IAF:
 
     def theta_term(self, theta: torch.Tensor) -> torch.Tensor:
         p = self._p
-        return _ThetaBranch.apply(theta, p("theta0/kernel"), p("theta0/bias"), p("theta1/kernel"),
-                                  p("theta1/bias"), p("theta2/kernel"), p("theta2/bias")).contiguous()
+        args = (theta, p("theta0/kernel"), p("theta0/bias"), p("theta1/kernel"), p("theta1/bias"), p("theta2/kernel"),
+                p("theta2/bias"))
+        self._fold = None
+        if (theta.is_cuda and theta.shape[1] <= 8 and max(a.shape[-1] for a in args[1:]) <= 64
+                and os.environ.get("VISSM_THETA_BRANCH_TORCH") != "1"):
+            tt, Wc, bc = _ThetaBranchK.apply(*args)
+            self._fold = (theta, Wc, bc)
+            return tt
+        return _ThetaBranch.apply(*args).contiguous()
 
     # ---- per-transition part (HIP) ----
     def weights(self):

@@ -95,6 +95,26 @@ def _dense_layout(t: torch.Tensor) -> bool:
     return True
 
 
+def theta_branch_fwd(theta, W0, b0, W1, b1, W2, b2, term: bool = True):
+    """The flows' theta-branch forward (include/vissm.h vissm_theta_branch_fwd; nma._ThetaBranchK): the collapsed
+    weights (Wc, bc) and, if term, theta_term = theta Wc + bc -- (theta_term or None, Wc, bc)."""
+    lib = _lib.load()
+    _require_gpu(W0, b0, W1, b1, W2, b2)
+    P, n0 = W0.shape
+    n1, H = W1.shape[1], W2.shape[1]
+    dev = W0.device
+    ws = [t.contiguous().float() for t in (W0, b0, W1, b1, W2, b2)]
+    Wc, bc = torch.empty(P, H, device=dev), torch.empty(H, device=dev)
+    tt, th, B = None, None, 0
+    if term:
+        th = theta.contiguous().float()
+        B = th.shape[0]
+        tt = torch.empty(B, H, device=dev)
+    check(lib.vissm_theta_branch_fwd(B, P, n0, n1, H, ptr(th), *[ptr(t) for t in ws], ptr(Wc), ptr(bc), ptr(tt),
+                                     _lib.stream_handle(dev)), "vissm_theta_branch_fwd")
+    return tt, Wc, bc
+
+
 def theta_branch_bwd(theta, d, W0, b0, W1, b1, W2):
     """The flows' theta-branch backward (include/vissm.h vissm_theta_branch_bwd; nma._ThetaBranch): dtheta and the
     gradients of (W0, b0, W1, b1, W2, b2) from d = d loss / d theta_term, in three launches."""
