@@ -591,17 +591,34 @@ __global__ __launch_bounds__(256) void theta_branch_fold_kernel(int P, int n0, i
   }
 }
 
-// theta_term[b][h] = theta[b] Wc[:, h] + bc[h] (one thread per output)
-__global__ __launch_bounds__(256) void theta_branch_term_kernel(int B, int P, int H, const float* __restrict__ theta,
+// theta_term[b][h] = theta[b] Wc[:, h] + bc[h]: lane h, each wave kTermRows rows with their loads in flight together
+constexpr int kTermRows = 16;
+template <int P>
+__global__ __launch_bounds__(256) void theta_branch_term_kernel(int B, int H, const float* __restrict__ theta,
                                                                  const float* __restrict__ Wc,
                                                                  const float* __restrict__ bc,
                                                                  float* __restrict__ out) {
-  const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= static_cast<size_t>(B) * H) return;
-  const int b = static_cast<int>(i / H), h = static_cast<int>(i % H);
-  float v = bc[h];
-  for (int p = 0; p < P; ++p) v += theta[static_cast<size_t>(b) * P + p] * Wc[p * H + h];
-  out[i] = v;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kTermRows, h = threadIdx.x & 63;
+  if (r0 >= B || h >= H) return;
+  float wc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) wc[p] = Wc[p * H + h];
+  const float c = bc[h];
+  float t[kTermRows][P];
+#pragma unroll
+  for (int i = 0; i < kTermRows; ++i) {
+    const int r = min(r0 + i, B - 1);
+#pragma unroll
+    for (int p = 0; p < P; ++p) t[i][p] = theta[r * P + p];
+  }
+#pragma unroll
+  for (int i = 0; i < kTermRows; ++i) {
+    if (r0 + i >= B) break;
+    float v = c;
+#pragma unroll
+    for (int p = 0; p < P; ++p) v += t[i][p] * wc[p];
+    out[static_cast<size_t>(r0 + i) * H + h] = v;
+  }
 }
 }  // namespace
 }  // namespace vissm
@@ -661,9 +678,15 @@ int vissm_theta_branch_fwd(int32_t B, int32_t P, int32_t n0, int32_t n1, int32_t
                      bc);
   VISSM_CHECK_LAUNCH("theta_branch_fold");
   if (theta_term && B > 0) {
-    const size_t n = static_cast<size_t>(B) * H;
-    hipLaunchKernelGGL(theta_branch_term_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st, B, P,
-                       H, theta, Wc, bc, theta_term);
+    const dim3 grid(static_cast<unsigned>((B + 4 * kTermRows - 1) / (4 * kTermRows)));
+    switch (P) {
+#define TT_CASE(PP)                                                                                         \
+  case PP:                                                                                                  \
+    hipLaunchKernelGGL(theta_branch_term_kernel<PP>, grid, dim3(256), 0, st, B, H, theta, Wc, bc, theta_term); \
+    break;
+      TT_CASE(1) TT_CASE(2) TT_CASE(3) TT_CASE(4) TT_CASE(5) TT_CASE(6) TT_CASE(7) TT_CASE(8)
+#undef TT_CASE
+    }
     VISSM_CHECK_LAUNCH("theta_branch_term");
   }
   return VISSM_OK;
