@@ -1,0 +1,18 @@
+#!/bin/bash
+# The paper-shape recovery run (scripts/ar_recovery.py, fp32, 10,000 steps) with the theta-branch kernels opt-in
+# (VISSM_THETA_BRANCH_KERNEL = 1: forward and backward kernels, bwd: backward kernel only) and with the default
+# torch form: which direction moves the posterior sd.  MODES / RUNS override the lists.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=$(pwd)/gpurun_out/rec; mkdir -p "$OUT"; export TMPDIR=/tmp
+for r in ${RUNS:-1}; do
+  for mode in ${MODES:-torch bwd 1}; do
+    if [ $mode = torch ]; then unset VISSM_THETA_BRANCH_KERNEL; else export VISSM_THETA_BRANCH_KERNEL=$mode; fi
+    echo "== $mode run $r"
+    timeout -k 10 200 python3 scripts/ar_recovery.py --steps 10000 --every 1000 > "$OUT/${mode}_$r.log" 2>&1 || exit 3
+    python3 -c "
+import json
+for l in open('$OUT/${mode}_$r.log'):
+    if l.startswith('{'):
+        d=json.loads(l); print(d['step'], [round(x,3) for x in d['mean']], [round(x,3) for x in d['sd']])"
+  done
+done

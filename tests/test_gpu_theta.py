@@ -130,8 +130,7 @@ def test_theta_branch_backward_kernel(B, P):
 @pytest.mark.parametrize("B,P", [(0, 3), (1, 3), (1000, 3), (65536, 3), (77, 8)])
 def test_theta_branch_forward_kernel(B, P):
     """vissm_theta_branch_fwd: the collapsed weights Wc = W0 W1 W2, bc = (b0 W1 + b1) W2 + b2 and theta_term =
-    theta Wc + bc against float64 (AR.py:63-68's three dense layers), and the GPU IAF path's theta_term / theta
-    gradient against the torch form of the same module (VISSM_THETA_BRANCH_TORCH=1)."""
+    theta Wc + bc against float64 (AR.py:63-68's three dense layers)."""
     from viforssms_amd.ops import theta_branch_fwd
     g = torch.Generator().manual_seed(B + 7 * P)
     r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
