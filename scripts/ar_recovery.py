@@ -45,7 +45,28 @@ def build(precision="fp32", seed=1):
     return model
 
 
-def run(steps=20000, every=1000, precision="fp32", graph=True, out=None, seed=1):
+def diagnostics(model):
+    """Optimiser and flow state behind a departure: the step's scalar summaries (ELBO terms, global norm), the
+    Adamax step ratio |v| / m (1 = a variable moving at the full learning rate), each flow's head bias (mu, sigma
+    pre-activation) and the largest |variable| per group."""
+    import torch
+    d = {k.split("/")[-1]: round(v, 4) for k, v in model.last.items()}
+    o = model._opt_main
+    r = (o.v.abs() / o.m.clamp_min(1e-30)).float()
+    d["adamax_ratio_mean"] = round(float(r.mean()), 4)
+    d["adamax_ratio_gt0.9"] = round(float((r > 0.9).float().mean()), 4)
+    st = model.store
+    for i in range(model.mdef.n_flows):
+        d[f"flow{i}_head_b"] = [round(float(x), 4) for x in st[f"flow{i}/head/bias"].detach().cpu()]
+    groups = {}
+    for n in st.names():
+        key = n.split("/")[0] + "/" + n.split("/")[1].rstrip("0123456789")
+        groups[key] = max(groups.get(key, 0.0), float(st[n].detach().abs().max()))
+    d["max_abs"] = {k: round(v, 3) for k, v in groups.items()}
+    return d
+
+
+def run(steps=20000, every=1000, precision="fp32", graph=True, out=None, seed=1, diag=False):
     model = build(precision, seed)
     t0 = time.time()
     model.train(None, None, max_runs=501, verbose=False, graph=False)   # pre-training (AR.py:290-298)
@@ -58,6 +79,8 @@ def run(steps=20000, every=1000, precision="fp32", graph=True, out=None, seed=1)
         done += n
         m, s = posterior(model)
         rec = {"step": done, "mean": m.tolist(), "sd": s.tolist(), "elapsed_s": round(time.time() - t0, 1)}
+        if diag:
+            rec["diag"] = diagnostics(model)
         recs.append(rec)
         print(json.dumps(rec), flush=True)
         if out:
@@ -73,5 +96,7 @@ if __name__ == "__main__":
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--seed", type=int, default=1, help="Philox seed of the eps / q(theta) base draws")
+    ap.add_argument("--diag", action="store_true", help="optimiser / flow diagnostics per record")
     a = ap.parse_args()
-    run(a.steps, a.every, a.precision, not a.no_graph, a.out)
+    run(a.steps, a.every, a.precision, not a.no_graph, a.out, a.seed, a.diag)

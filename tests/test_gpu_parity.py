@@ -11,7 +11,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-from tests.parity_util import run_parity_case, build_model, emulated_tol  # noqa: E402
+from tests.parity_util import run_parity_case, build_model, emulated_tol, EMUL_CAP  # noqa: E402
 from oracle import nma_oracle as O  # noqa: E402
 from viforssms_amd import _lib  # noqa: E402
 
@@ -78,10 +78,11 @@ def test_family_parity_multi_window(family, k, T, starts):
 BF16X3_TOL = dict(elbo_tol=1e-4, grad_tol=1e-3, param_tol=2e-2)
 
 
-def _check_emulated(res):
-    tol = emulated_tol(res)
+def _check_emulated(res, cap=None):
+    tol = emulated_tol(res, cap=cap)
     print("emulated", {k: v for k, v in res["emul"].items() if k != "per_param"},
-          "-> elbo %.2e grad %.2e" % (tol["elbo_tol"], tol["grad_tol"]))
+          "-> effective bars elbo %.2e grad %.2e param <= %.2e" % (tol["elbo_tol"], tol["grad_tol"],
+                                                                  max(tol["param_tol"].values())))
     _check(res, **tol)
 
 
@@ -110,9 +111,10 @@ def test_ar_parity_matrix_core_paper_and_multiwindow():
     starts = [0, 50, 100, 100, 250, 0]
     _check(run_parity_case("ar", 6, 50, 10, 3, 32, 3, 10, device=DEV, T=300, starts=starts, precision=2), **BF16X3_TOL)
     # several windows at bf16x2: the one-sample backward kernel with split weights (bwd_kernel<..., NP = 2>); this
-    # case's ELBO (~ -6.8e3) is a cancellation of terms ~100x larger, which the emulated bar reflects
+    # case's ELBO (~ -6.8e3) is a cancellation of terms ~100x larger, which the emulated bar reflects (capped at bf16's
+    # earlier bar, which held this case in round 4)
     _check_emulated(run_parity_case("ar", 6, 50, 10, 3, 32, 3, 10, device=DEV, T=300, starts=starts,
-                                    precision=_lib.VISSM_PREC_BF16X2, emulate=True))
+                                    precision=_lib.VISSM_PREC_BF16X2, emulate=True), cap=EMUL_CAP["bf16"])
 
 
 # LV / SV / FHN heads (3 hidden layers, BN folded into the next layer) on the bf16 kernels

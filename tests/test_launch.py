@@ -36,6 +36,7 @@ def test_launch_command_rendezvous_on_loopback():
 def test_plain_python_gpus_2_spawns_two_ranks(tmp_path):
     env = {k: v for k, v in os.environ.items() if k not in DIST_VARS}
     env["PYTHONPATH"] = ROOT
+    env["VISSM_DIST_BACKEND"] = "gloo"   # CPU host (an empty HIP_VISIBLE_DEVICES list refuses an RCCL world)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_launch_probe.py"), "--gpus", "2", str(tmp_path)],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -63,6 +64,10 @@ def test_launcher_never_touches_the_gpu_runtime(monkeypatch):
     assert len(calls) == 1 and "--nproc-per-node=2" in calls[0]
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
     with pytest.raises(SystemExit, match="needs 2 visible GPUs"):
+        launch.ensure_world(2, "b.py", [])
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")               # an explicitly empty list is zero devices
+    assert launch.visible_gpu_count() == 0
+    with pytest.raises(SystemExit, match="found 0"):
         launch.ensure_world(2, "b.py", [])
     monkeypatch.setenv("VISSM_DIST_BACKEND", "gloo")            # the one-GPU rehearsal may oversubscribe
     assert launch.ensure_world(2, "b.py", []) == 0

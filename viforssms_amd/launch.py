@@ -20,16 +20,23 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def visible_gpu_count() -> int:
+def visible_gpu_count() -> Optional[int]:
     """GPUs this process could hand to its ranks, WITHOUT touching the GPU runtime (torch.cuda.device_count() may
     initialise HIP on this torch build, and a launcher must not spawn its ranks from a process that did): the
-    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list when one is set, else the DRM render
-    nodes.  0 = unknown."""
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list when one is set (an empty list is zero
+    devices), else the AMD (vendor 0x1002) DRM render nodes.  None = unknown."""
     for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
             return len([d for d in v.split(",") if d.strip() != ""])
-    return len(glob.glob("/dev/dri/renderD*"))
+    n = 0
+    for node in glob.glob("/sys/class/drm/renderD*"):
+        try:
+            with open(os.path.join(node, "device", "vendor")) as f:
+                n += int(f.read().strip(), 16) == 0x1002
+        except (OSError, ValueError):
+            continue
+    return n or None
 
 
 def rank_launch_cmd(gpus: int, script: str, argv: List[str], port: Optional[int] = None) -> List[str]:
@@ -55,7 +62,7 @@ def ensure_world(gpus: int, script: str, argv: List[str]) -> Optional[int]:
         return None
     n_dev = visible_gpu_count()   # no torch.cuda here: the ranks are spawned from this process
     backend = os.environ.get("VISSM_DIST_BACKEND", "nccl")
-    if 0 < n_dev < gpus and backend != "gloo":
+    if n_dev is not None and n_dev < gpus and backend != "gloo":
         raise SystemExit(f"--gpus {gpus} needs {gpus} visible GPUs for RCCL, found {n_dev} "
                          "(VISSM_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
     return subprocess.call(rank_launch_cmd(gpus, script, argv))

@@ -79,7 +79,8 @@ def _theta_branch_kernels(which: str) -> bool:
     that run further still, so the run is sensitive to last-bit rounding; until the recovery check is robust to that,
     the library-GEMM form whose trajectory it was tuned on stays the default.  "fwd" / "bwd"
     turn on one direction only (the forward kernel also runs the backward kernel)."""
-    return os.environ.get("VISSM_THETA_BRANCH_KERNEL") in ("1", which, "fwd" if which == "bwd" else "")
+    v = os.environ.get("VISSM_THETA_BRANCH_KERNEL")
+    return v == "1" or v == which or (which == "bwd" and v == "fwd")
 
 
 class _ThetaBranchK(torch.autograd.Function):
@@ -281,7 +282,7 @@ class IAF:
         forms (the same fp32 products), passed to the flow kernels as constants (VissmFlowParams.theta_rank) so
         the two-sample AR kernels form the theta term inside their layer-0 product; the gradient still flows
         through theta_term."""
-        st = getattr(self, "_fold", None)
+        st, self._fold = getattr(self, "_fold", None), None   # consumed here: no graph or weights kept past the step
         if st is not None and st[0] is theta:   # the collapsed weights theta_term was just formed with
             return theta.detach().contiguous(), st[1], st[2]
         p = self._p
@@ -618,6 +619,7 @@ class Engine:
         theta_term).  VISSM_THETA_FOLD=0 turns it off (A/B)."""
         if (self.mdef.family != "ar" or self.precision == _lib.VISSM_PREC_FP32 or theta.shape[1] > 5
                 or os.environ.get("VISSM_THETA_FOLD", "1") == "0"):
+            fl._fold = None   # the theta-branch kernel's collapsed weights go unused: drop them (and theta's graph)
             return None
         return fl.theta_factors(theta)
 
