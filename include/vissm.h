@@ -233,6 +233,13 @@ typedef struct {
                                 shift 0 (the state is softplus(z) / z itself: the reference's windows pin x_0 only,
                                 lotka_volterra_partial.py:381-384, SV_dense.py:322-328); NULL: mask / shift read
                                 everywhere.  vissm_elbo_fwd_grad skips their loads and the general transform there. */
+  const int32_t* obs_list;   /* LV / FHN, optional [n_win][obs_stride]: the elements e in [1, M] whose observation row
+                                e - 1 has a nonzero obs_bin in either coordinate, ascending, padded with -1 (the
+                                reference's obs_bin files are sparse: dat/LV_obs_binary.txt, loaded at
+                                lotka_volterra_partial.py:481-487, observes every 100th step; fitz_nag_NVP.py:468-473
+                                loads its own); NULL: the obs rows are read at every element.  With it
+                                vissm_elbo_fwd_grad evaluates the observation term at the listed elements only. */
+  int32_t obs_stride;        /* entries per window in obs_list */
 } VissmElboData;
 
 int vissm_elbo_fwd(const VissmElboDesc* d, const VissmElboData* data,

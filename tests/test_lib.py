@@ -77,19 +77,24 @@ def test_feature_kernels_refuse_kernel_shorter_than_stride():
 
 def test_elbo_fwd_grad_checks_without_gpu():
     """vissm_elbo_fwd_grad (the training step's one-pass log-density call): a null z / dz is refused and B = 0 is a
-    no-op, before any device work; VissmElboData carries plain_from as its last field (include/vissm.h)."""
+    no-op, before any device work; VissmElboData carries the observation list as its last fields (include/vissm.h)."""
     from viforssms_amd import _lib
     lib = _lib.load()
-    assert [f[0] for f in _lib.ElboData._fields_][-1] == "plain_from"
+    assert [f[0] for f in _lib.ElboData._fields_][-2:] == ["obs_list", "obs_stride"]
     fake = ctypes.c_void_p(16)   # never dereferenced: the checks run first
     d = _lib.ElboDesc(_lib.MODEL_FHN, 4, 10, 1, 0.1, 1.0)
-    data = _lib.ElboData(None, fake, fake, None, None, None, None)
+    data = _lib.ElboData(None, fake, fake, None, None, None, None, None, 0)
     rc = lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(data), None, fake, fake, fake, None, fake, fake,
                                  None, fake, fake, None)
     assert rc < 0 and b"null pointer" in lib.vissm_last_error()
     d0 = _lib.ElboDesc(_lib.MODEL_FHN, 0, 10, 1, 0.1, 1.0)
     assert lib.vissm_elbo_fwd_grad(ctypes.byref(d0), ctypes.byref(data), fake, fake, fake, fake, None, fake, fake,
                                    None, fake, fake, None) == 0
+    # an observation list without its stride is refused before any launch
+    bad = _lib.ElboData(None, fake, fake, None, None, None, None, fake, 0)
+    rc = lib.vissm_elbo_fwd_grad(ctypes.byref(d), ctypes.byref(bad), fake, fake, fake, fake, None, fake, fake,
+                                 None, fake, fake, None)
+    assert rc < 0 and b"obs_stride" in lib.vissm_last_error()
 
 
 def test_bf16x2_precisions_without_gpu():
@@ -272,7 +277,7 @@ def test_abi_struct_layouts_match_ctypes():
     f.restype = None
     f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
     for which, (cls, last) in enumerate([(_lib.FlowDesc, "out_pitch"), (_lib.FlowParams, "theta_rank"),
-                                         (_lib.FlowGrads, "b_head")]):
+                                         (_lib.FlowGrads, "b_head"), (_lib.ElboData, "obs_stride")]):
         out = (ctypes.c_size_t * 2)()
         f(which, out)
         assert out[0] == ctypes.sizeof(cls), (cls.__name__, out[0], ctypes.sizeof(cls))

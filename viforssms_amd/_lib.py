@@ -84,7 +84,8 @@ class ThetaDesc(ctypes.Structure):
 
 
 class ElboData(ctypes.Structure):
-    _fields_ = [(n, _c_void_p) for n in ("win", "obs", "obs_bin", "mask", "shift", "dim_one", "plain_from")]
+    _fields_ = [(n, _c_void_p) for n in ("win", "obs", "obs_bin", "mask", "shift", "dim_one", "plain_from",
+                                        "obs_list")] + [("obs_stride", ctypes.c_int32)]
 
 
 # exported symbol -> (restype, argtypes); tests check that every symbol of include/vissm.h is here

@@ -642,7 +642,9 @@ __device__ __forceinline__ float lane_val(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
-template <int MODEL>
+// OL (VissmElboData.obs_list): the observation term leaves the chunk loop and the element-wise tail (no obs / obs_bin
+// row loads there) and is evaluated after them at the window's listed elements only, its dz added to the stored one.
+template <int MODEL, bool OL = false>
 __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float* __restrict__ z,
                                                              const float* __restrict__ theta,
                                                              const float* __restrict__ g_sde,
@@ -676,7 +678,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     for (int i = 0; i < P; ++i) acc[i] += on * r.gth[i];
   };
   // the obs row e - 1 observing x_e (e >= 1): gradient into g, value into the sums
-  auto obs_g = [&](const St& s, float y0, float y1, float b0, float b1, float* g, float on) {
+  auto obs_term = [&](const St& s, float y0, float y1, float b0, float b1, float* g, float on) {
     if constexpr (Dv::kObs) {
       const float d0 = s.x[0] - y0, d1 = s.x[1] - y1;
       g[0] += cgo * b0 * d0;
@@ -684,6 +686,9 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
       s_q += on * (b0 * (d0 * isd) * (d0 * isd) + b1 * (d1 * isd) * (d1 * isd));
       s_b += on * (b0 + b1);
     }
+  };
+  auto obs_g = [&](const St& s, float y0, float y1, float b0, float b1, float* g, float on) {
+    if constexpr (!OL) obs_term(s, y0, y1, b0, b1, g, on);
   };
   // dz of element s from its state gradient g (+ the ILDJ term observing it, e >= 1)
   auto dz_of = [&](const St& s, const float* g, bool ildj, float on, float* o) {
@@ -725,7 +730,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     St st[kV];
     m.template states<kV, PLAIN>(zb, t0, st);
     float y[2][kV], bb[2][kV];
-    if constexpr (Dv::kObs) {  // rows t0 - 1 .. t0 + kV - 2 observe x_{t0} .. x_{t0+kV-1}
+    if constexpr (Dv::kObs && !OL) {  // rows t0 - 1 .. t0 + kV - 2 observe x_{t0} .. x_{t0+kV-1}
       ldn<kV>(m.ob + t0 - 1, y[0]);
       ldn<kV>(m.ob + M + t0 - 1, y[1]);
       ldn<kV>(m.bn + t0 - 1, bb[0]);
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
         hpend0 = tl.gh[0];
         hpend1 = tl.gh[1];
       }
-      if constexpr (Dv::kObs)
+      if constexpr (Dv::kObs && !OL)
         obs_g(sc, m.ob[t - 1], m.ob[M + t - 1], m.bn[t - 1], m.bn[M + t - 1], g, 1.f);
     }
     float o[ZD];
@@ -883,6 +888,28 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
 #pragma unroll
       for (int i = 0; i < ZD * kV; i += 4)
         *reinterpret_cast<f4u*>(dzb + ZD * pt0 + i) = f4u{pend[i], pend[i + 1], pend[i + 2], pend[i + 3]};
+    }
+  }
+  if constexpr (Dv::kObs && OL) {
+    // the listed observed elements: the obs term's value and its dz, added to the element's stored dz (g enters dz
+    // linearly through d x / d z).  This wave wrote every element of its row above: its stores complete first.
+    __threadfence_block();
+    const int os = a.d.obs_stride;
+    const int* ol = a.d.obs_list + static_cast<size_t>(w) * os;
+    for (int r0 = 0; r0 < os; r0 += 64) {
+      const int e = r0 + lane < os ? ol[r0 + lane] : -1;
+      if (e >= 1 && e <= M) {
+        const St sc = m.state(zb, e);
+        float g[2] = {0.f, 0.f};
+        obs_term(sc, m.ob[e - 1], m.ob[M + e - 1], m.bn[e - 1], m.bn[M + e - 1], g, 1.f);
+        if constexpr (ZD == 2) {
+          float* p2 = dzb + 2 * e;
+          const f2u v = *reinterpret_cast<const f2u*>(p2);
+          *reinterpret_cast<f2u*>(p2) = f2u{v[0] + g[0] * sc.j[0], v[1] + g[1] * sc.j[1]};
+        } else {
+          dzb[e] += g[1] * sc.j[1];
+        }
+      }
     }
   }
 #pragma unroll
@@ -1237,10 +1264,12 @@ int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const
   if (rc) return rc;
   VISSM_CHECK_ARG(z && theta && sde && dz && dtheta, "elbo_fwd_grad: null pointer");
   if (d->B == 0) return VISSM_OK;
+  VISSM_CHECK_ARG(!data->obs_list || data->obs_stride > 0, "elbo_fwd_grad: obs_list needs obs_stride > 0");
   Args a = make(d, data);
   hipStream_t st = as_stream(stream);
   dim3 grid((d->B + kSW - 1) / kSW), blk(256);
   const Vals vo{sde, obs, extra};
+  const bool ol = data->obs_list != nullptr && (d->model == VISSM_MODEL_LV || d->model == VISSM_MODEL_FHN);
   prof_begin(VISSM_PROF_ELBO_BWD, st);
   switch (d->model) {
     case VISSM_MODEL_AR:
@@ -1248,9 +1277,19 @@ int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const
                          g_obs, dz, dtheta, vo);
       break;
 #if VISSM_ELBO_ONEPASS_NB
-    case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    case VISSM_MODEL_LV:
+      if (ol)
+        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      else
+        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_SV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
-    default: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    default:
+      if (ol)
+        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      else
+        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      break;
 #else
     case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_SV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;

@@ -29,13 +29,14 @@ float vissm_host_sp_ildj(float y, float* gy) { return vissm::em::sp_ildj(y, gy);
 float vissm_host_obs(float x, float y, float bin, float sd, float* gx) { return vissm::em::obs_term(x, y, bin, sd, gx); }
 
 // the C ABI's struct layouts as the C compiler sees them (the ctypes mirrors in viforssms_amd/_lib.py are
-// checked against these): which = 0 VissmFlowDesc, 1 VissmFlowParams, 2 VissmFlowGrads; out = {size, offset of
-// the last field}
+// checked against these): which = 0 VissmFlowDesc, 1 VissmFlowParams, 2 VissmFlowGrads, 3 VissmElboData; out = {size,
+// offset of the last field}
 void vissm_host_abi_layout(int which, size_t* out) {
   switch (which) {
     case 0: out[0] = sizeof(VissmFlowDesc); out[1] = offsetof(VissmFlowDesc, out_pitch); break;
     case 1: out[0] = sizeof(VissmFlowParams); out[1] = offsetof(VissmFlowParams, theta_rank); break;
-    default: out[0] = sizeof(VissmFlowGrads); out[1] = offsetof(VissmFlowGrads, b_head); break;
+    case 2: out[0] = sizeof(VissmFlowGrads); out[1] = offsetof(VissmFlowGrads, b_head); break;
+    default: out[0] = sizeof(VissmElboData); out[1] = offsetof(VissmElboData, obs_stride); break;
   }
 }
 

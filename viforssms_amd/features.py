@@ -11,6 +11,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+import os
+
 import numpy as np
 
 
@@ -145,6 +147,22 @@ def plain_from_table(mask_vals, shift_vals, M: int) -> np.ndarray:
     return np.where(ld >= s, ld - s + 1, 0).astype(np.int32)
 
 
+def obs_list_table(obs_bin, M: int) -> np.ndarray:
+    """VissmElboData.obs_list per window start s (int32 [n_starts, stride]): the elements e in [1, M] of the window
+    [s, s + M] whose observation row e - 1 (obs_bin[:, s + e - 1]) is nonzero in either coordinate, ascending,
+    padded with -1 -- the one-pass ELBO kernel evaluates the observation term there only (the reference's
+    observations are sparse: every 100th LV step, lotka_volterra_partial.py:481-487)."""
+    ob = np.atleast_2d(obs_bin)
+    hit = (ob != 0).any(0)
+    n = max(hit.size - M + 1, 1)
+    rows = [np.flatnonzero(hit[s:s + M]) + 1 for s in range(n)]
+    stride = max(1, max(len(r) for r in rows))
+    out = np.full((n, stride), -1, dtype=np.int32)
+    for s, r in enumerate(rows):
+        out[s, :len(r)] = r
+    return out
+
+
 class DeviceTable:
     """The FeatureTable's padded channel arrays (and the per-window feed tables) resident on the GPU,
     built once per model; ``batch(uniq_dev, n)`` gathers time_feats and the ELBO feeds of n window
@@ -165,6 +183,7 @@ class DeviceTable:
         self.extra = {}
         if tab.family in ("lv", "fhn"):
             self.extra["obs_bin"] = f32(ex["obs_bin"])
+            self.obs_list = torch.as_tensor(obs_list_table(ex["obs_bin"], tab.M), device=device)
         if tab.family in ("lv", "sv"):
             self.extra["mask"] = f32(ex["mask_vals"])
             self.extra["shift"] = f32(ex["shift_vals"])
@@ -209,4 +228,6 @@ class DeviceTable:
             feeds["dim_one"] = out
         if t.family in ("lv", "sv"):
             feeds["plain_from"] = self.plain_from[uniq_dev.long()]
+        if t.family in ("lv", "fhn") and os.environ.get("VISSM_ELBO_OBS_LIST", "1") != "0":
+            feeds["obs_list"] = self.obs_list[uniq_dev.long()].contiguous()
         return ts, feeds

@@ -419,10 +419,15 @@ class ElboFeeds:
     win: Optional[torch.Tensor] = None
     n_win: int = 1
     plain_from: Optional[torch.Tensor] = None   # int32 [n_win]: VissmElboData.plain_from (None: NULL)
+    obs_list: Optional[torch.Tensor] = None     # int32 [n_win, stride]: VissmElboData.obs_list (None: NULL)
 
     def cdata(self) -> ElboData:
+        ol = self.obs_list
+        if ol is not None and (ol.dtype != torch.int32 or ol.dim() != 2 or not ol.is_contiguous()
+                               or ol.shape[0] != self.n_win or ol.shape[1] < 1):
+            raise ValueError("obs_list must be a contiguous int32 [n_win, stride >= 1] tensor")
         return ElboData(ptr(self.win), ptr(self.obs), ptr(self.obs_bin), ptr(self.mask), ptr(self.shift),
-                        ptr(self.dim_one), ptr(self.plain_from))
+                        ptr(self.dim_one), ptr(self.plain_from), ptr(ol), int(ol.shape[1]) if ol is not None else 0)
 
 
 class ElboFn(torch.autograd.Function):
@@ -507,7 +512,8 @@ def elbo_values_grad(model: int, M: int, dt: float, obs_std: float, feeds: ElboF
     (vissm_elbo_fwd_grad): the training step knows these upstream gradients before the forward.  No autograd: the
     caller feeds dz / dtheta into a multi-root backward (Engine.forward_onepass)."""
     lib = _lib.load()
-    _require_gpu(z, theta, g_sde, feeds.obs, feeds.obs_bin, feeds.mask, feeds.shift, feeds.dim_one, feeds.win)
+    _require_gpu(z, theta, g_sde, feeds.obs, feeds.obs_bin, feeds.mask, feeds.shift, feeds.dim_one, feeds.win,
+                 feeds.plain_from, feeds.obs_list)
     B = z.shape[0]
     d = ElboDesc(model, B, M, feeds.n_win, float(dt), float(obs_std))
     data = feeds.cdata()
