@@ -187,7 +187,8 @@ def test_ar_posterior_trajectory_matches_oracle(prec):
 
 
 RECOVERY_STEPS = int(os.environ.get("VISSM_RECOVERY_STEPS", "10000"))
-from tests.recovery_util import RECOVERY_EVERY, RECOVERY_SEEDS, RECOVERY_SPAN, longest_band_run  # noqa: E402
+from tests.recovery_util import (RECOVERY_BY, RECOVERY_EVERY, RECOVERY_SEEDS, RECOVERY_SPAN,  # noqa: E402
+                                 first_in_band, longest_band_run)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
@@ -198,14 +199,15 @@ def test_ar_posterior_recovers_generating_theta(prec):
     import ar_recovery
     cwd = os.getcwd()
     os.chdir(ROOT)
-    spans = {}
+    spans, firsts = {}, {}
     try:
         for seed in RECOVERY_SEEDS[prec]:
             _, recs = ar_recovery.run(steps=RECOVERY_STEPS, every=RECOVERY_EVERY, precision=prec, seed=seed)
-            spans[seed] = longest_band_run(recs)
-            print(f"seed {seed}: longest run in the band {spans[seed]} checkpoints; trajectory:",
+            spans[seed], firsts[seed] = longest_band_run(recs), first_in_band(recs)
+            print(f"seed {seed}: in the band from step {firsts[seed]}, longest run {spans[seed]} checkpoints; trajectory:",
                   [(r["step"], np.round(r["mean"], 3).tolist(), np.round(r["sd"], 3).tolist())
                    for r in recs if r["step"] % 1000 == 0], flush=True)
     finally:
         os.chdir(cwd)
     assert all(v >= RECOVERY_SPAN for v in spans.values()), (spans, RECOVERY_SPAN)
+    assert all(f is not None and f <= RECOVERY_BY for f in firsts.values()), (firsts, RECOVERY_BY)

@@ -15,10 +15,13 @@
 // (deterministic; no atomics).
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace vissm {
 namespace feat {
 
-constexpr int kT = 32;     // output positions per block (forward) / per m-range of a block (backward)
+// output positions per block (forward) / per m-range of a block (backward): KT = 32, or 16 where the 32-position grid
+// would leave most CUs idle (AR-cfg: one window of 5017 positions is 157 blocks for 256 CUs; pick_kt)
 constexpr int kNT = 256;   // 4 waves: lane = output unit, wave = row group
 constexpr int kMaxH = 64, kMaxCin = 63, kMaxK = 64;
 
@@ -78,9 +81,11 @@ __device__ void dense_elu(const float* in, int ip, int nin, const float* Ws, int
 // LDS layout (floats) shared by both kernels: rows padded to the next multiple of 32
 __host__ __device__ inline int rows_pad(int r) { return (r + 31) / 32 * 32; }
 
-// forward: grid (ceil(Lh / kT), n_win)
+// forward: grid (ceil(Lh / KT), n_win)
+template <int KT>
 __global__ __launch_bounds__(kNT) void feat_fwd_kernel(Args a, Params p, const float* __restrict__ h0,
                                                        float* __restrict__ C, float* __restrict__ act) {
+  constexpr int kT = KT, RQ = KT / 4;   // output rows per wave in the conv
   extern __shared__ float sm[];
   const int H = a.H, hp = H + 1, ip = a.Cin + 1;
   const int w = blockIdx.y, m0 = blockIdx.x * kT;
@@ -118,29 +123,29 @@ __global__ __launch_bounds__(kNT) void feat_fwd_kernel(Args a, Params p, const f
   dense_elu(hB, hp, H, Ws, hp, p.b[3], hA, hp, R, H, ab + 3 * plane, n_own);   // F in hA (pitch hp)
   // rows of hA at and past R hold the previous layer's values: zero them (the conv reads up to RP rows)
   for (int idx = threadIdx.x; idx < (RP - R) * hp; idx += kNT) hA[R * hp + idx] = 0.f;
-  // the conv over the feature channels: thread (o, rg) owns output rows rg*8 .. rg*8 + 7
+  // the conv over the feature channels: thread (o, rg) owns output rows rg*RQ .. rg*RQ + RQ - 1
   const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  float acc[8];
+  float acc[RQ];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  for (int q = 0; q < RQ; ++q) acc[q] = 0.f;
   for (int j = 0; j < a.k; ++j) {
     __syncthreads();
     stage_tap(Ws, hp, p.cw, j, H);
     __syncthreads();
     if (o < H) {
-      const float* Fr = hA + (a.s * rg * 8 + j) * hp;
+      const float* Fr = hA + (a.s * rg * RQ + j) * hp;
       for (int i = 0; i < H; ++i) {
         const float wv = Ws[i * hp + o];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] = fmaf(Fr[a.s * q * hp + i], wv, acc[q]);
+        for (int q = 0; q < RQ; ++q) acc[q] = fmaf(Fr[a.s * q * hp + i], wv, acc[q]);
       }
     }
   }
   if (o < H) {
     const float bo = p.cb[o];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int m = rg * 8 + q;
+    for (int q = 0; q < RQ; ++q) {
+      const int m = rg * RQ + q;
       if (m < nm) C[(static_cast<size_t>(w) * a.Lh + m0 + m) * H + o] = acc[q] + bo;
     }
   }
@@ -186,11 +191,13 @@ __device__ void wgrad(const float* X, int xp, int nin, const float* G, int gp, i
   }
 }
 
-// backward: grid (ceil(Lu / (s kT)), n_win); block b owns F rows [b s kT, (b + 1) s kT) and positions
-// m in [b kT, (b + 1) kT)
+// backward: grid (ceil(Lu / (s KT)), n_win); block b owns F rows [b s KT, (b + 1) s KT) and positions
+// m in [b KT, (b + 1) KT)
+template <int KT>
 __global__ __launch_bounds__(kNT) void feat_bwd_kernel(Args a, Params p, const float* __restrict__ h0,
                                                        const float* __restrict__ act, const float* __restrict__ dC,
                                                        float* __restrict__ slab) {
+  constexpr int kT = KT;
   extern __shared__ float sm[];
   const int H = a.H, hp = H + 1, ip = a.Cin + 1, k = a.k, s = a.s;
   const int w = blockIdx.y, b = blockIdx.x;
@@ -247,21 +254,22 @@ __global__ __launch_bounds__(kNT) void feat_bwd_kernel(Args a, Params p, const f
       }
   }
   // dF[r][i] = sum_j sum_o dC[(r - j) / s][o] W_j[i][o] over (r - j) divisible by s: thread (i, rg) rows
-  // rg*8 .. rg*8 + 7 of each 32-row group
-  {
+  // rg*Q .. rg*Q + Q - 1 of each 4Q-row group (Q = 8, or 4 when the block owns 16 rows)
+  auto dF_pass = [&](auto qtag) {
+    constexpr int Q = decltype(qtag)::value;
     const int i = o;
-    for (int rb = 0; rb < TR; rb += 32) {
-      float acc[8];
+    for (int rb = 0; rb < TR; rb += 4 * Q) {
+      float acc[Q];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+      for (int q = 0; q < Q; ++q) acc[q] = 0.f;
       for (int j = 0; j < k; ++j) {
         __syncthreads();
         stage_tap(Ws, hp, p.cw, j, H);
         __syncthreads();
         if (i < H) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int r = r0 + rb + rg * 8 + q - j;    // s m for the tap's position m
+          for (int q = 0; q < Q; ++q) {
+            const int r = r0 + rb + rg * Q + q - j;    // s m for the tap's position m
             if (r % s != 0) continue;                    // wave-uniform (one row per wave and q)
             const int mi = (r >= 0 ? r / s : -((-r + s - 1) / s)) - m_lo;
             if (mi < 0 || mi >= nd) continue;
@@ -275,13 +283,18 @@ __global__ __launch_bounds__(kNT) void feat_bwd_kernel(Args a, Params p, const f
       // dz4 = dF * elu'(F) (F from the staged rows: row r - r0 of Fs)
       if (i < H) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int rl = rb + rg * 8 + q;
+        for (int q = 0; q < Q; ++q) {
+          const int rl = rb + rg * Q + q;
           if (rl < GP) G0[rl * hp + i] = rl < nr ? acc[q] * elu_d_out(Fs[rl * hp + i]) : 0.f;
         }
       }
     }
-  }
+    // rows [4Q ceil(TR / 4Q), GP) stay for the MLP backward below to read as zeros
+    for (int rl = (TR + 4 * Q - 1) / (4 * Q) * (4 * Q) + threadIdx.x / 64; rl < GP; rl += 4)
+      if (i < H) G0[rl * hp + i] = 0.f;
+  };
+  if (TR >= 32) dF_pass(std::integral_constant<int, 8>{});
+  else dF_pass(std::integral_constant<int, 4>{});
   // the MLP backward, layer 3 down to 0: dW_l = X_l^T dz, db_l = sum dz, dz_prev = (dz W_l^T) * elu'(X_l)
   float* Gc = G0;
   float* Gn = G1;
@@ -358,11 +371,18 @@ __global__ void feat_scatter_kernel(const float* __restrict__ red, int Cin, int 
   }
 }
 
-static size_t fwd_smem(const Args& a) {
+// 16 output positions per block where 32 would give fewer than two blocks per CU
+static int pick_kt(const Args& a) {
+  const int64_t nb32 = static_cast<int64_t>((a.Lh + 31) / 32) * a.n_win;
+  return nb32 < 512 ? 16 : 32;
+}
+static int bwd_blocks(const Args& a, int kT) { return (a.Lu + a.s * kT - 1) / (a.s * kT); }
+
+static size_t fwd_smem(const Args& a, int kT) {
   const int RP = rows_pad(a.s * (kT - 1) + a.k), hp = a.H + 1, wp = std::max(a.Cin, a.H) + 1;
   return static_cast<size_t>(RP * wp + RP * hp + wp * hp) * sizeof(float);
 }
-static size_t bwd_smem(const Args& a) {
+static size_t bwd_smem(const Args& a, int kT) {
   const int hp = a.H + 1, ip = a.Cin + 1;
   const int nd = kT + (a.k - 1 + a.s - 1) / a.s + 1;   // upper bound of the staged dC rows
   const int DP = rows_pad(nd), FP = rows_pad(a.s * (kT - 1) + a.k), GP = rows_pad(a.s * kT);
@@ -373,11 +393,12 @@ static size_t bwd_smem(const Args& a) {
 // dynamic LDS above the default 64 KB (the backward at k = 20 / 50 takes 70-85 KB): raise the kernels' limit once
 static int allow_lds() {
   static int rc = [] {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(feat_fwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(feat_bwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return 1;
+    const void* fs[4] = {reinterpret_cast<const void*>(feat_fwd_kernel<16>),
+                         reinterpret_cast<const void*>(feat_fwd_kernel<32>),
+                         reinterpret_cast<const void*>(feat_bwd_kernel<16>),
+                         reinterpret_cast<const void*>(feat_bwd_kernel<32>)};
+    for (const void* f : fs)
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return 1;
     return 0;
   }();
   return rc;
@@ -427,7 +448,7 @@ extern "C" {
 size_t vissm_feat_workspace_size(const VissmFeatDesc* d) {
   feat::Args a;
   if (feat::make(d, &a)) return 0;
-  const int nb = (a.Lu + a.s * feat::kT - 1) / (a.s * feat::kT);
+  const int nb = feat::bwd_blocks(a, feat::pick_kt(a));
   const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
   return align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)) + align_up(of.n * sizeof(float));
 }
@@ -442,9 +463,14 @@ int vissm_feat_fwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
     set_error("feat_fwd: hipFuncSetAttribute failed");
     return VISSM_ELAUNCH;
   }
-  dim3 grid((a.Lh + feat::kT - 1) / feat::kT, a.n_win);
-  hipLaunchKernelGGL(feat::feat_fwd_kernel, grid, dim3(feat::kNT), feat::fwd_smem(a), as_stream(stream), a,
-                     feat::params(w), h0, C, act);
+  const int kt = feat::pick_kt(a);
+  dim3 grid((a.Lh + kt - 1) / kt, a.n_win);
+  if (kt == 16)
+    hipLaunchKernelGGL(feat::feat_fwd_kernel<16>, grid, dim3(feat::kNT), feat::fwd_smem(a, 16), as_stream(stream), a,
+                       feat::params(w), h0, C, act);
+  else
+    hipLaunchKernelGGL(feat::feat_fwd_kernel<32>, grid, dim3(feat::kNT), feat::fwd_smem(a, 32), as_stream(stream), a,
+                       feat::params(w), h0, C, act);
   VISSM_CHECK_LAUNCH("feat_fwd");
   return VISSM_OK;
 }
@@ -461,13 +487,18 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
     return VISSM_ELAUNCH;
   }
   hipStream_t st = as_stream(stream);
-  const int nb = (a.Lu + a.s * feat::kT - 1) / (a.s * feat::kT);
+  const int kt = feat::pick_kt(a);
+  const int nb = feat::bwd_blocks(a, kt);
   const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
   float* slab = static_cast<float*>(workspace);
   float* red = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                         align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)));
-  hipLaunchKernelGGL(feat::feat_bwd_kernel, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a), st, a,
-                     feat::params(w), h0, act, dC, slab);
+  if (kt == 16)
+    hipLaunchKernelGGL(feat::feat_bwd_kernel<16>, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a, 16), st, a,
+                       feat::params(w), h0, act, dC, slab);
+  else
+    hipLaunchKernelGGL(feat::feat_bwd_kernel<32>, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a, 32), st, a,
+                       feat::params(w), h0, act, dC, slab);
   VISSM_CHECK_LAUNCH("feat_bwd");
   rc = launch_reduce_rows(slab, red, static_cast<int64_t>(a.n_win) * nb, of.n, st);
   if (rc) return rc;
