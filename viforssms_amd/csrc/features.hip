@@ -15,6 +15,7 @@
 // (deterministic; no atomics).
 #include "common.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace vissm {
@@ -294,7 +295,8 @@ __global__ __launch_bounds__(kNT) void feat_bwd_kernel(Args a, Params p, const f
       if (i < H) G0[rl * hp + i] = 0.f;
   };
   if (TR >= 32) dF_pass(std::integral_constant<int, 8>{});
-  else dF_pass(std::integral_constant<int, 4>{});
+  else if (TR >= 16) dF_pass(std::integral_constant<int, 4>{});
+  else dF_pass(std::integral_constant<int, 2>{});
   // the MLP backward, layer 3 down to 0: dW_l = X_l^T dz, db_l = sum dz, dz_prev = (dz W_l^T) * elu'(X_l)
   float* Gc = G0;
   float* Gn = G1;
@@ -371,8 +373,17 @@ __global__ void feat_scatter_kernel(const float* __restrict__ red, int Cin, int 
   }
 }
 
-// 16 output positions per block where 32 would give fewer than two blocks per CU
-static int pick_kt(const Args& a) {
+// output positions per block: 32, or 16 where 32 would give fewer than two blocks per CU (forward: fewer positions
+// per block recompute more halo rows, k - s per block); VISSM_FEAT_KT / VISSM_FEAT_KT_BWD = 8 | 16 | 32 override
+// (A/B timing; the backward's choice also sizes its workspace: set it before vissm_feat_workspace_size)
+static int env_kt(const char* name) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : 0;
+  return (v == 8 || v == 16 || v == 32) ? v : 0;
+}
+static int pick_kt(const Args& a, bool bwd) {
+  const int forced = env_kt(bwd ? "VISSM_FEAT_KT_BWD" : "VISSM_FEAT_KT");
+  if (forced) return forced;
   const int64_t nb32 = static_cast<int64_t>((a.Lh + 31) / 32) * a.n_win;
   return nb32 < 512 ? 16 : 32;
 }
@@ -393,8 +404,10 @@ static size_t bwd_smem(const Args& a, int kT) {
 // dynamic LDS above the default 64 KB (the backward at k = 20 / 50 takes 70-85 KB): raise the kernels' limit once
 static int allow_lds() {
   static int rc = [] {
-    const void* fs[4] = {reinterpret_cast<const void*>(feat_fwd_kernel<16>),
+    const void* fs[6] = {reinterpret_cast<const void*>(feat_fwd_kernel<8>),
+                         reinterpret_cast<const void*>(feat_fwd_kernel<16>),
                          reinterpret_cast<const void*>(feat_fwd_kernel<32>),
+                         reinterpret_cast<const void*>(feat_bwd_kernel<8>),
                          reinterpret_cast<const void*>(feat_bwd_kernel<16>),
                          reinterpret_cast<const void*>(feat_bwd_kernel<32>)};
     for (const void* f : fs)
@@ -448,7 +461,7 @@ extern "C" {
 size_t vissm_feat_workspace_size(const VissmFeatDesc* d) {
   feat::Args a;
   if (feat::make(d, &a)) return 0;
-  const int nb = feat::bwd_blocks(a, feat::pick_kt(a));
+  const int nb = feat::bwd_blocks(a, feat::pick_kt(a, true));
   const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
   return align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)) + align_up(of.n * sizeof(float));
 }
@@ -463,9 +476,12 @@ int vissm_feat_fwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
     set_error("feat_fwd: hipFuncSetAttribute failed");
     return VISSM_ELAUNCH;
   }
-  const int kt = feat::pick_kt(a);
+  const int kt = feat::pick_kt(a, false);
   dim3 grid((a.Lh + kt - 1) / kt, a.n_win);
-  if (kt == 16)
+  if (kt == 8)
+    hipLaunchKernelGGL(feat::feat_fwd_kernel<8>, grid, dim3(feat::kNT), feat::fwd_smem(a, 8), as_stream(stream), a,
+                       feat::params(w), h0, C, act);
+  else if (kt == 16)
     hipLaunchKernelGGL(feat::feat_fwd_kernel<16>, grid, dim3(feat::kNT), feat::fwd_smem(a, 16), as_stream(stream), a,
                        feat::params(w), h0, C, act);
   else
@@ -487,13 +503,16 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
     return VISSM_ELAUNCH;
   }
   hipStream_t st = as_stream(stream);
-  const int kt = feat::pick_kt(a);
+  const int kt = feat::pick_kt(a, true);
   const int nb = feat::bwd_blocks(a, kt);
   const feat::Off of = feat::offsets(a.Cin, a.H, a.k);
   float* slab = static_cast<float*>(workspace);
   float* red = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                         align_up(static_cast<size_t>(a.n_win) * nb * of.n * sizeof(float)));
-  if (kt == 16)
+  if (kt == 8)
+    hipLaunchKernelGGL(feat::feat_bwd_kernel<8>, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a, 8), st, a,
+                       feat::params(w), h0, act, dC, slab);
+  else if (kt == 16)
     hipLaunchKernelGGL(feat::feat_bwd_kernel<16>, dim3(nb, a.n_win), dim3(feat::kNT), feat::bwd_smem(a, 16), st, a,
                        feat::params(w), h0, act, dC, slab);
   else
