@@ -5,4 +5,4 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out/svflag; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 300 python3 scripts/sv_case_errs.py sv50 --all > "$OUT/tree.log" 2>&1 || exit 3
 VISSM_LIB=$(pwd)/abl/lib_sv5vgpr.so timeout -k 10 300 python3 scripts/sv_case_errs.py sv50 --all > "$OUT/vgpr.log" 2>&1 || exit 4
-tail -3 "$OUT/tree.log" "$OUT/vgpr.log"
+tail -n 3 "$OUT/tree.log"; tail -n 3 "$OUT/vgpr.log"

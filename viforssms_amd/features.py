@@ -228,6 +228,9 @@ class DeviceTable:
             feeds["dim_one"] = out
         if t.family in ("lv", "sv"):
             feeds["plain_from"] = self.plain_from[uniq_dev.long()]
-        if t.family in ("lv", "fhn") and os.environ.get("VISSM_ELBO_OBS_LIST", "1") != "0":
+        # the observation list is opt-in (VISSM_ELBO_OBS_LIST=1): its post-pass (a fence, then a read-modify-write of
+        # dz at every listed element) measured slower than reading the obs rows at every element -- LV one-pass
+        # 0.390 -> 0.397 ms, FHN 0.075 -> 0.127 ms (observations every 100th / 10th step; profiles/r06/ab_r06b.log)
+        if t.family in ("lv", "fhn") and os.environ.get("VISSM_ELBO_OBS_LIST", "0") == "1":
             feeds["obs_list"] = self.obs_list[uniq_dev.long()].contiguous()
         return ts, feeds
