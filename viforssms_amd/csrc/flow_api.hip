@@ -6,6 +6,8 @@
 // and it measured slower (LV-like shape: 64 vs 76 ms bwd).  No process state.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace vissm {
 
 size_t flow2_workspace_size(const VissmFlowDesc* d, int backward);
@@ -102,9 +104,19 @@ static bool use_v5(const VissmFlowDesc* d) { return d->precision != VISSM_PREC_F
 // builds without the SLP vectorizer (LV-cfg backward 18.1 -> 16.8 ms, FHN 3.7 -> 3.5, SV 7.2 -> 6.7 ms per launch),
 // k <= 24 in flow_v5n.hip (also VGPR-form MFMAs and AGPR accumulators: LV 16.6 -> 14.6 ms), k > 32 in flow_v5s.hip.
 // The one-sample three-layer kernel (several windows) measured slower without the vectorizer (SV: 10.3 -> 10.8 ms).
-static bool use_nh3(const VissmFlowDesc* d) { return d->n_hidden == 3 && d->n_win == 1 && d->k <= 24; }
+// VISSM_NH3_DEFAULT_FORM=1 sends the k <= 24 shapes to flow_v5s.hip's build as well (the same source without the
+// VGPR-form flag and the asm accumulators): tests/test_gpu_vgpr_form.py checks that flow_v5n.hip's kernels compute what
+// that build computes at every shape they ship for -- the flag miscompiled SV's k = 50 du variant
+static bool nh3_default_form() {
+  const char* e = std::getenv("VISSM_NH3_DEFAULT_FORM");
+  return e && e[0] == '1';
+}
+static bool use_nh3(const VissmFlowDesc* d) {
+  return d->n_hidden == 3 && d->n_win == 1 && d->k <= 24 && !nh3_default_form();
+}
 static bool use_nh3s(const VissmFlowDesc* d) {
-  return d->n_hidden == 3 && d->n_win == 1 && d->k > 32 && d->k <= 64 && !d->stride2;
+  return d->n_hidden == 3 && d->n_win == 1 && d->k <= 64 &&
+         ((d->k > 32 && !d->stride2) || (d->k <= 24 && nh3_default_form()));
 }
 
 }  // namespace vissm

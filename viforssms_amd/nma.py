@@ -269,10 +269,12 @@ class IAF:
         VISSM_FEAT_TORCH=1 selects the torch form everywhere, VISSM_FEAT_MAX_K moves the kernel_len bound (A/B timing)."""
         f = self.spec.feat
         kmax = int(os.environ.get("VISSM_FEAT_MAX_K", "16"))
-        if (ts.is_cuda and f == "mlp4" and s <= self.spec.k <= kmax
+        if (ts.is_cuda and f in ("mlp4", "sv") and s <= self.spec.k <= kmax
                 and os.environ.get("VISSM_FEAT_TORCH") != "1"):   # vissm_feat_* need kernel_len >= stride
             p = self._p
-            return feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
+            # SV's MLP input is the features with their first differences (SV_dense.py:53): formed here, data only
+            h0 = ts[:, :-1, :] if f == "mlp4" else torch.cat([ts[:, 1:, :], ts[:, 1:, :-2] - ts[:, :-1, :-2]], 2)
+            return feat_conv(h0, s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
                              p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
                              p("conv/kernel"), p("conv/bias"))
         return self.conv_shared(self.features(ts), Lh, s, gemm=gemm)
