@@ -21,8 +21,8 @@
 namespace vissm {
 namespace feat {
 
-// output positions per block (forward) / per m-range of a block (backward): KT = 32, or 16 where the 32-position grid
-// would leave most CUs idle (AR-cfg: one window of 5017 positions is 157 blocks for 256 CUs; pick_kt)
+// output positions per block (forward) / per m-range of a block (backward): KT = 32, 16 or 8, fewer where the
+// 32-position grid would leave most CUs idle (AR-cfg: one window of 5017 positions is 157 blocks for 256 CUs; pick_kt)
 constexpr int kNT = 256;   // 4 waves: lane = output unit, wave = row group
 constexpr int kMaxH = 64, kMaxCin = 63, kMaxK = 64;
 
@@ -373,9 +373,11 @@ __global__ void feat_scatter_kernel(const float* __restrict__ red, int Cin, int 
   }
 }
 
-// output positions per block: 32, or 16 where 32 would give fewer than two blocks per CU (forward: fewer positions
-// per block recompute more halo rows, k - s per block); VISSM_FEAT_KT / VISSM_FEAT_KT_BWD = 8 | 16 | 32 override
-// (A/B timing; the backward's choice also sizes its workspace: set it before vissm_feat_workspace_size)
+// output positions per block: the largest of 32 / 16 / 8 that still gives two blocks per CU, else 8 (forward: fewer
+// positions per block recompute more halo rows, k - s per block).  Same-box A/B (profiles/r06/ab_r06b.log,
+// ab_r06d.log): FHN-cfg step 14.08 (torch form) -> 14.20 (16) -> 13.88 ms (8); AR-cfg 79.11 (16) / 78.82 (32) /
+// 78.61 ms (8), within noise.  VISSM_FEAT_KT / VISSM_FEAT_KT_BWD = 8 | 16 | 32 override (A/B timing; the backward's
+// choice also sizes its workspace: set it before vissm_feat_workspace_size)
 static int env_kt(const char* name) {
   const char* e = std::getenv(name);
   const int v = e ? std::atoi(e) : 0;
@@ -384,8 +386,9 @@ static int env_kt(const char* name) {
 static int pick_kt(const Args& a, bool bwd) {
   const int forced = env_kt(bwd ? "VISSM_FEAT_KT_BWD" : "VISSM_FEAT_KT");
   if (forced) return forced;
-  const int64_t nb32 = static_cast<int64_t>((a.Lh + 31) / 32) * a.n_win;
-  return nb32 < 512 ? 16 : 32;
+  for (int kt = 32; kt > 8; kt /= 2)
+    if (static_cast<int64_t>((a.Lh + kt - 1) / kt) * a.n_win >= 512) return kt;
+  return 8;
 }
 static int bwd_blocks(const Args& a, int kT) { return (a.Lu + a.s * kT - 1) / (a.s * kT); }
 

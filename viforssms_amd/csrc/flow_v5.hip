@@ -456,7 +456,7 @@ __device__ __forceinline__ void fence() { asm volatile("" ::: "memory"); }
 // registers 12.5, both from LDS 12.9 ms against 11.6).  The backward keeps its fences between phases: at ~250
 // VGPRs nothing may be hoisted.
 //
-// Backward design decisions (A/B measurements): one hidden layer -- the head gradient rides in
+// Backward design decisions (A/B measurements, docs/DESIGN_HISTORY.md §4 / §8): one hidden layer -- the head gradient rides in
 // the dZ image (no G fragment via LDS), elu'(I_0) from the bf16 pairs the recompute keeps in registers, the dX and
 // dcon weight fragments, dW's I_0 and dW_eps's u fragments all read before the head-backward VALU block; the dW /
 // dW_head MFMAs (off the unit's critical path) issued after the du section's dcon stores (105.6 -> 104.3 ms per
@@ -1319,7 +1319,7 @@ __device__ __forceinline__ float swap_hi_lo(float v) {
   return __builtin_bit_cast(float, static_cast<unsigned>(r[1]));
 }
 constexpr int KP2 = 8;  // carry slots / dcon rows (k <= 8)
-// Design decisions (A/B, AR-cfg launches):
+// Design decisions (A/B, AR-cfg launches; docs/DESIGN_HISTORY.md §4 / §8):
 //  * compiler fences between the unit's phases in the fused (FZ) variant (without them: middle flows 23.3 ->
 //    22.4 ms, the fused one 26.8 -> 28.2, the first flow unchanged) and, since round 5, in the first flow's variant
 //    without du (18.31 -> 18.07 ms; the middle flows with them 20.57 -> 20.88: profiles/r05/ab_sched_strategies.log);

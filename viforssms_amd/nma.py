@@ -260,15 +260,16 @@ class IAF:
         return (_DiagSum.apply(G.contiguous(), Lh, s) + self._p("conv/bias")).contiguous()
 
     def window_conv(self, ts: torch.Tensor, Lh: int, s: int, gemm: Optional[str] = None) -> torch.Tensor:
-        """C = conv_shared(features(ts)): the first conv's window-shared part.  On the GPU, at kernel_len <= 16
-        (the AR configurations), the feature branch (a few thousand rows of [14] -> 50 -> 50 -> 50 -> 50, then the
-        k-tap conv) runs as one HIP launch each way (ops.feat_conv, vissm_feat_fwd / _bwd) instead of ~40 torch
-        launches per flow: AR-cfg step -0.25 ms.  The FHN (k = 20, stride 2) and SV (k = 50) shapes keep the library
-        GEMMs: their conv is a K = k H = 1000 / 2500 contraction the fp32 VALU kernel runs slower (FHN step +1.0 ms,
-        SV +6.1 ms, profiles/r04/ab_feat.log), and so do LV's time-mixing features ([kernel_ext - 1] channels).
-        VISSM_FEAT_TORCH=1 selects the torch form everywhere, VISSM_FEAT_MAX_K moves the kernel_len bound (A/B timing)."""
+        """C = conv_shared(features(ts)): the first conv's window-shared part.  On the GPU, at kernel_len <= 24 (the AR
+        configurations and FHN's k = 20, stride 2), the feature branch (a few thousand rows of [C] -> 50 -> 50 -> 50 ->
+        50, then the k-tap conv) runs as one HIP launch each way (ops.feat_conv, vissm_feat_fwd / _bwd) instead of ~40
+        torch launches per flow: AR-cfg step -0.25 ms; FHN-cfg 14.08 -> 13.88 ms at 8 positions per block (round 6;
+        at 32 per block, round 4, it had lost to the torch form by 1 ms).  SV's k = 50 (its diff-augmented input goes
+        through the same kernels) measured 43.6 -> 44.8 ms and keeps the library GEMMs, as does LV's time-mixing
+        feature layer ([kernel_ext - 1] channels).  VISSM_FEAT_TORCH=1 selects the torch form everywhere,
+        VISSM_FEAT_MAX_K moves the kernel_len bound (A/B timing)."""
         f = self.spec.feat
-        kmax = int(os.environ.get("VISSM_FEAT_MAX_K", "16"))
+        kmax = int(os.environ.get("VISSM_FEAT_MAX_K", "24"))
         if (ts.is_cuda and f in ("mlp4", "sv") and s <= self.spec.k <= kmax
                 and os.environ.get("VISSM_FEAT_TORCH") != "1"):   # vissm_feat_* need kernel_len >= stride
             p = self._p
