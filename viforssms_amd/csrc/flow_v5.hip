@@ -232,6 +232,37 @@ __device__ __forceinline__ float elu_fast(float x) {
 __device__ __forceinline__ float elu_d(float y) {
   return __builtin_fmaf(__builtin_amdgcn_fmed3f(y, -3.0e38f, 0.f), kLn2, 1.f);
 }
+// The two-sample backward kernels take elu' from the recompute itself: the exponential clamped to [0, 1] (the clamp
+// folds into v_exp_f32) IS the derivative, min(2^x', 1), and with it the ELU is max(x', log2(e)(d - 1)) -- the same
+// three instructions as elu_fast<true>, bitwise the same value.  d is kept as f16 pairs (v_cvt_pk_f16_f32: 2^-11
+// relative, below the bf16 rounding the products apply next) and applied by v_fma_mix_f32 (fp32 x f16 half, one
+// instruction per element) instead of re-deriving elu' from the activation (unpack, med3, fma, mul: four).
+// Levels: 0 off, 1 elu'(A0) only (in the registers of the bf16 A0 pairs it replaces), 2 every level (AR; LV / FHN at
+// k <= 32 in the first flow's variant without du).  The pair unit issues 7 % (AR) / 15 % (LV) fewer instructions, but
+// the kernels are latency-bound, so the time moves little: first measured slower (AR-cfg middle-flow backward 20.4 ->
+// 23.2 ms) because the scheduler sank the packing to the pairs' use and spilled an accumulator in the loop
+// (profiles/r06/ab_r06e.log); with the pairs pinned where they are computed (pin_pair) and flow_v5 / flow_v5f built
+// without the SLP vectorizer (which otherwise unpacks the halves for v_pk_fma_f32 instead of v_fma_mix_f32): AR-cfg
+// step 79.6 -> 79.3 ms (first flow 18.3 -> 17.9, middle 20.65 -> 20.47, fused unchanged), LV no-du backward 12.8 ->
+// 12.2 ms but the du variant 15.8 -> 16.6 (off there), FHN alike (profiles/r06/ab_r06g.log).
+#ifndef VISSM_DERIV16
+#define VISSM_DERIV16 2
+#endif
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float elu_dv(float x, float& d) {
+  d = __builtin_amdgcn_fmed3f(__builtin_amdgcn_exp2f(x), 0.f, 1.f);
+  return __builtin_amdgcn_fmed3f(x, __builtin_fmaf(kLog2e, d, -kLog2e), 3.0e38f);
+}
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, h2v));
+}
+// materialise a pair where it is computed (left alone, the scheduler sinks the packing to the pair's use and keeps the
+// fp32 derivatives live across the recompute's MFMA chains instead: a spilled accumulator in the loop)
+__device__ __forceinline__ void pin_pair(u2& v) { asm volatile("" : "+v"(v[0]), "+v"(v[1])); }
+// x * (f16 half `half` of pk) as v_fma_mix_f32 (a plain product would unpack first)
+__device__ __forceinline__ float mul_h(float x, unsigned pk, int half) {
+  return __builtin_fmaf(x, static_cast<float>(__builtin_bit_cast(h2v, pk)[half]), 0.f);
+}
 // (the forward kernels take log sigma on v_log_f32: sigma >= 1e-10 is a normal float; AR-cfg fwd 7.56 -> 7.34 ms)
 // softplus on v_exp_f32 / v_log_f32 directly (__logf adds a denormal-scaling and refinement sequence; 1 + e^-|x|
 // lies in [1, 2]) and max(x, 0) as a median
@@ -336,8 +367,16 @@ __host__ __device__ __forceinline__ int fold_index(int kk, int R, int* which) {
 }
 __device__ __forceinline__ float bf16_hi(float x) { return static_cast<float>(static_cast<__bf16>(x)); }
 
+#ifndef VISSM_NO_LOFOLD
+#define VISSM_NO_LOFOLD 0  // (A/B switch: 1 keeps the separate lo MFMAs)
+#endif
+constexpr bool kLoFoldOff = VISSM_NO_LOFOLD;
+// lofold (the two-sample kernels' split-weight products, k <= 8): the lo planes of the layer-0 and head weights ride in
+// the hi plane's otherwise zero rows -- layer-0 K rows 8..15 (lane group 1, whose B operand then repeats the taps
+// 0..7) and head output rows 4q + 2, 4q + 3 (lo of mu, r: the kernel adds d[2], d[3] to d[0], d[1]) -- so those
+// products need no second MFMA (kLoFold below)
 __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int NP, int KB, int JB,
-                            bf8* __restrict__ img, float* __restrict__ cst, int fold) {
+                            bf8* __restrict__ img, float* __restrict__ cst, int fold, int lofold) {
   const int f = blockIdx.x, lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   const int NPL = NP >= 2 ? 2 : 1;
   float v[8];
@@ -357,7 +396,10 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
       const int kb = r >> 2, ob = r & 3;
       const int jt = 32 * kb + 8 * g + j, h = swz(16 * ob + c);
       if (jt < k && h < H) x = w.w_eps[jt * H + h] * kLog2e;
-      else if (fold && kb == 0 && jt >= kFoldRow && h < H) {  // the theta term's rows (theta fold)
+      else if (lofold && kb == 0 && jt >= 8 && jt < 16 && jt - 8 < k && h < H) {  // lo of the taps 0..7
+        const float wv = w.w_eps[(jt - 8) * H + h] * kLog2e;
+        x = wv - bf16_hi(wv);
+      } else if (fold && kb == 0 && jt >= kFoldRow && h < H) {  // the theta term's rows (theta fold)
         int which;
         const int i = fold_index(jt - kFoldRow, w.theta_rank, &which);
         if (i >= 0) {
@@ -377,6 +419,8 @@ __global__ void prep_kernel(VissmFlowParams w, int H, int k, int nh, int bn, int
       const int o = c & 3;
       if (o < 2 && h < H) x = wt_head(w, H, bn, nh, h, o) * kLn2;
       else if (o < 2 && h == HP - 1) x = bias_head(w, H, bn, nh, o);
+      else if (lofold && h < H) x = wt_head(w, H, bn, nh, h, o - 2) * kLn2 - bf16_hi(wt_head(w, H, bn, nh, h, o - 2) * kLn2);
+      else if (lofold && h == HP - 1) x = bias_head(w, H, bn, nh, o - 2) - bf16_hi(bias_head(w, H, bn, nh, o - 2));
     }
     v[j] = x;
   }
@@ -1372,6 +1416,7 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
                                                       const u4* __restrict__ thf, FzArgs fz = FzArgs{}) {
   static_assert(!SB || NPR == 2, "the split backward chain goes with the split recompute");
   constexpr int NH = 1, KB = 1, JB = 1, NP = 1;
+  constexpr bool LOF = NPR == 2 && !kLoFoldOff;  // the recompute's layer-0 / head lo products in spare rows (k <= 8)
   constexpr int PO = FZ ? P - 1 : P;
   constexpr int QW2 = P + KP2;  // dcon[j][p] stored at column p + j: du[q] = sum_j row_j[q], no masks
   // u window entries: the layer-0 fragment reads up to c + 8 g + 7 <= 46 (48 in the split-weight variants, whose
@@ -1522,11 +1567,13 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       }
       // ---- forward recompute of both samples (shared weight fragments)
       u2 i0p[2][4];
+      u2 d0p[2][4], d1p[2][4];  // VISSM_DERIV16: elu'(A0), elu'(A1) as f16 pairs
       float mu[2], rr[2];
       {
         f4 acc[2][4];
         fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
-        Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, g, c), u_frag<NP>(uwin[w][1], 1, 0, g, c)};
+        const int gu = (LOF && g == 1) ? 0 : g;  // LOF: lane group 1's K rows repeat the taps 0..7 (lo weights)
+        Fr8<NP> uf[2] = {u_frag<NP>(uwin[w][0], 1, 0, gu, c), u_frag<NP>(uwin[w][1], 1, 0, gu, c)};
         if constexpr (TF) {
           if (g >= 2) {
             uf[0].h = tfr[0];
@@ -1537,23 +1584,32 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
         for (int ob = 0; ob < 4; ++ob) {
           const Fr8<NP> wf = wfrag(sh, 16 * NH + ob, lane);
           bf8 wel = {};
-          if constexpr (NPR == 2) {
+          if constexpr (NPR == 2 && !LOF) {
             const bf8 v = swe[ob][c];
             if (g == 0) wel = v;
           }
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             acc[cb][ob] = X[cb][ob];
-            if constexpr (NPR == 2) acc[cb][ob] = mfma32(wel, uf[cb].h, acc[cb][ob]);
+            if constexpr (NPR == 2 && !LOF) acc[cb][ob] = mfma32(wel, uf[cb].h, acc[cb][ob]);
             acc[cb][ob] = mm<NP>(wf, uf[cb], acc[cb][ob]);
           }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb) {
+            float e[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              if (VISSM_DERIV16 >= 1) X[cb][rb][r] = 4 * rb + r < NR ? elu_dv(acc[cb][rb][r], e[r]) : 0.f;
+              else X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            }
+            if (VISSM_DERIV16 >= 1) {
+              d0p[cb][rb] = u2{pk_f16(e[0], e[1]), 4 * rb + 2 < NR ? pk_f16(e[2], e[3]) : 0u};
+              pin_pair(d0p[cb][rb]);
+            }
+          }
         fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -1577,15 +1633,26 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           put_image<NP>(im0 + cb * P * HP, nullptr, X[cb], g, c);  // I_0 with its ones row
+          if (VISSM_DERIV16 == 0) {
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb) i0p[cb][rb] = u2{cvt2(X[cb][rb][0], X[cb][rb][1]), cvt2(X[cb][rb][2], X[cb][rb][3])};
+            for (int rb = 0; rb < 4; ++rb) i0p[cb][rb] = u2{cvt2(X[cb][rb][0], X[cb][rb][1]), cvt2(X[cb][rb][2], X[cb][rb][3])};
+          }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb) {
+            float e[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              if (VISSM_DERIV16 >= 2) X[cb][rb][r] = 4 * rb + r < NR ? elu_dv(acc[cb][rb][r], e[r]) : 0.f;
+              else X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+            }
+            if (VISSM_DERIV16 >= 2) {
+              d1p[cb][rb] = u2{pk_f16(e[0], e[1]), 4 * rb + 2 < NR ? pk_f16(e[2], e[3]) : 0u};
+              pin_pair(d1p[cb][rb]);
+            }
+          }
         fence2<FZ || (!DU && VISSM_NODU_FENCES)>();
         const int fh = 16 * NH + 4 * KB + 2 * JB;
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -1598,14 +1665,14 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
             const Fr8<NP> xk = chain_frag<NP>(X[cb], ks);
-            if constexpr (NPR == 2) d[cb] = mfma32(slo[8 + ks][lane], xk.h, d[cb]);
+            if constexpr (NPR == 2 && !LOF) d[cb] = mfma32(slo[8 + ks][lane], xk.h, d[cb]);
             d[cb] = mm<NP>(wf, xk, d[cb]);
           }
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          mu[cb] = d[cb][0];
-          rr[cb] = d[cb][1];
+          mu[cb] = LOF ? d[cb][0] + d[cb][2] : d[cb][0];
+          rr[cb] = LOF ? d[cb][1] + d[cb][3] : d[cb][1];
           put_image<NP>(im1 + cb * P * HP, nullptr, X[cb], g, c);  // I_1 (head input) with its ones row
         }
       }
@@ -1743,8 +1810,10 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              if (VISSM_DERIV16 >= 2) D[cb][rb][r] = 4 * rb + r < NR ? mul_h(D[cb][rb][r], d1p[cb][rb][r >> 1], r & 1) : 0.f;
+              else D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+            }
           put_image<NP>(im1 + cb * P * HP, nullptr, D[cb], g, c);
         }
       }
@@ -1786,10 +1855,15 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const f4 x = {__builtin_bit_cast(float, i0p[cb][rb][0] << 16), __builtin_bit_cast(float, i0p[cb][rb][0] & 0xffff0000u),
-                        __builtin_bit_cast(float, i0p[cb][rb][1] << 16), __builtin_bit_cast(float, i0p[cb][rb][1] & 0xffff0000u)};
+          if (VISSM_DERIV16 >= 1) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? mul_h(dX[cb][rb][r], d0p[cb][rb][r >> 1], r & 1) : 0.f;
+          } else {
+            const f4 x = {__builtin_bit_cast(float, i0p[cb][rb][0] << 16), __builtin_bit_cast(float, i0p[cb][rb][0] & 0xffff0000u),
+                          __builtin_bit_cast(float, i0p[cb][rb][1] << 16), __builtin_bit_cast(float, i0p[cb][rb][1] & 0xffff0000u)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+          }
         }
       // dcon[j][p] = sum_h w_eps[j][h] dA0[h][p] per sample; the dC tile += dA0 of both
       f4 dcn[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -2007,7 +2081,8 @@ __global__ __launch_bounds__(NT2, 2) void bwd2_kernel(KArgs a, const float* __re
 // forward): hi planes register-resident, lo planes read from LDS per use
 // NH / JB: one hidden layer (AR) or three with the BN affine folded (LV / SV / FHN heads: stride-2 head with the
 // pass-through of the even outputs and the fused pair swap), k <= 32 (one layer-0 K block)
-template <bool TF, int NP, int NH, int JB, int NWF = NW>
+// LOF (NP = 2, k <= 8: prep_kernel's lofold): the layer-0 and head lo products ride in the hi fragments' spare rows
+template <bool TF, int NP, int NH, int JB, int NWF = NW, bool LOF = false>
 __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float* __restrict__ u,
                                                                   const float* __restrict__ C,
                                                                   const float* __restrict__ tht,
@@ -2106,7 +2181,8 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
       {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          bf8 uf[2] = {u_frag<1>(uwin[w][0], ss, kb, g, c).h, u_frag<1>(uwin[w][1], ss, kb, g, c).h};
+          const int gu = (LOF && g == 1) ? 0 : g;  // LOF: lane group 1's K rows repeat the taps 0..7 (lo weights)
+          bf8 uf[2] = {u_frag<1>(uwin[w][0], ss, kb, gu, c).h, u_frag<1>(uwin[w][1], ss, kb, gu, c).h};
           if constexpr (TF) {
             if (g >= 2) {
               uf[0] = tfr[0];
@@ -2115,9 +2191,15 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
           }
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob) {
-            const Fr8<NP> wf = W(16 * NH + 4 * kb + ob, 8 * NH + 4 * kb + ob);
+            if constexpr (LOF) {
+              const bf8 wh = HIREG ? wr[8 * NH + 4 * kb + ob] : sh.img[16 * NH + 4 * kb + ob][0][lane];
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
+              for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mfma32(wh, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
+            } else {
+              const Fr8<NP> wf = W(16 * NH + 4 * kb + ob, 8 * NH + 4 * kb + ob);
+#pragma unroll
+              for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mmw(wf, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
+            }
           }
         }
       }
@@ -2159,9 +2241,22 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
       f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const Fr8<NP> wf = W(fh + ks, 8 * NH + 4 * KB + ks);
+        if constexpr (LOF) {
+          const bf8 wh = HIREG ? wr[8 * NH + 4 * KB + ks] : sh.img[fh + ks][0][lane];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) d[cb] = mmw(wf, chain_frag<1>(X[cb], ks).h, d[cb]);
+          for (int cb = 0; cb < 2; ++cb) d[cb] = mfma32(wh, chain_frag<1>(X[cb], ks).h, d[cb]);
+        } else {
+          const Fr8<NP> wf = W(fh + ks, 8 * NH + 4 * KB + ks);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) d[cb] = mmw(wf, chain_frag<1>(X[cb], ks).h, d[cb]);
+        }
+      }
+      if constexpr (LOF) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          d[cb][0] += d[cb][2];
+          d[cb][1] += d[cb][3];
+        }
       }
       if (g == 0 && c < nP) {
 #pragma unroll
@@ -2228,6 +2323,9 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
   // copies those operands between register files around the statements (scripts/check_agpr_asm.py finds the copies
   // within an MFMA's wait states), so the builtin form stays there
   constexpr bool AACC = VISSM_BWD2N_AACC && JB <= 2;
+  // elu' as f16 pairs (VISSM_DERIV16) at k <= 32 in the variant without du (with du: LV 15.8 -> 16.6 ms per launch);
+  // SV's k > 32 build has no registers to spare for them
+  constexpr bool DV = VISSM_DERIV16 >= 2 && JB <= 2 && !DU;
   constexpr int KR = JB == 1 ? 16 : JB == 2 ? 24 : KP;
   constexpr int QWR = DIAG ? P + 1 : s * P + KR;
   constexpr int UWN = KB == 1 ? 64 : 128;    // u entries staged per sample (s P + k of them read)
@@ -2318,6 +2416,25 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
       }
       // ---- forward recompute of both samples; I_0 .. I_NH kept as bf16 pairs (with the ones row)
       u2 ip[NH + 1][2][4];
+      u2 dp[DV ? NH + 1 : 1][2][4];  // DV: elu'(I_0 .. I_NH) as f16 pairs (VISSM_DERIV16)
+      // the ELU of both samples' accumulators, with (DV) its derivative pairs
+      auto elu_pairs = [&](const f4 (&ac)[2][4], f4 (&Y)[2][4], u2 (&dd)[2][4]) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            float e[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (DV) Y[cb][rb][r] = 4 * rb + r < NR ? elu_dv(ac[cb][rb][r], e[r]) : 0.f;
+              else Y[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(ac[cb][rb][r]) : 0.f;
+            }
+            if constexpr (DV) {
+              dd[cb][rb] = u2{pk_f16(e[0], e[1]), 4 * rb + 2 < NR ? pk_f16(e[2], e[3]) : 0u};
+              pin_pair(dd[cb][rb]);
+            }
+          }
+      };
       float mu[2], rr[2];
       {
         f4 acc[2][4];
@@ -2332,12 +2449,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
             for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, uf[cb], kb == 0 ? X[cb][ob] : acc[cb][ob]);
           }
         }
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+        elu_pairs(acc, X, dp[0]);
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
           fence();
@@ -2360,13 +2472,7 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
               for (int cb = 0; cb < 2; ++cb) acc[cb][ob] = mm<NP>(wf, xf[cb], acc[cb][ob]);
             }
           }
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                X[cb][rb][r] = 4 * rb + r < NR ? elu_fast<true>(acc[cb][rb][r]) : 0.f;
+          elu_pairs(acc, X, dp[l + 1]);
         }
         fence();
         f4 d[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -2440,7 +2546,10 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (DV) D[cb][rb][r] = 4 * rb + r < NR ? mul_h(D[cb][rb][r], dp[NH][cb][rb][r >> 1], r & 1) : 0.f;
+              else D[cb][rb][r] = 4 * rb + r < NR ? D[cb][rb][r] * elu_d(X[cb][rb][r]) : 0.f;
+            }
       }
       // ---- hidden layers, top down: D = dZ_l; dW_l += I_l D^T; D <- (W_l D) * elu'(I_l)
 #pragma unroll
@@ -2486,9 +2595,15 @@ __global__ __launch_bounds__(NT3, 1) void bwd2n_kernel(KArgs a, const float* __r
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 4; ++rb) {
-            const f4 x = unpack_pair(ip[l][cb][rb]);
+            if constexpr (DV) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+              for (int r = 0; r < 4; ++r)
+                D[cb][rb][r] = 4 * rb + r < NR ? mul_h(dX[cb][rb][r], dp[l][cb][rb][r >> 1], r & 1) : 0.f;
+            } else {
+              const f4 x = unpack_pair(ip[l][cb][rb]);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) D[cb][rb][r] = 4 * rb + r < NR ? dX[cb][rb][r] * elu_d(x[r]) : 0.f;
+            }
           }
       }
       // ---- D = dA0: dC tile, dcon, dW_eps, d theta
@@ -2957,6 +3072,11 @@ static bool fold_ok(const VissmFlowDesc* d, const VissmFlowParams* w) {
          d->k <= kFoldRow && d->n_hidden == 1;
 }
 
+// the split-weight (bf16x2) two-sample kernels' layer-0 / head lo products in the hi fragments' spare rows (prep_kernel)
+static bool lofold_ok(const VissmFlowDesc* d) {
+  return np_of(d) == 2 && d->k <= 8 && d->n_hidden == 1 && !kLoFoldOff;
+}
+
 // padded C (+ b_theta when folding) and either the padded theta term or the theta fold's B-operand rows
 static void launch_pad(const VissmFlowDesc* d, const VissmFlowParams* w, const Geom& g, const float* C,
                        const float* tht, const Ws& ws, bool fold, hipStream_t st) {
@@ -2971,10 +3091,11 @@ static void launch_pad(const VissmFlowDesc* d, const VissmFlowParams* w, const G
                        nT, d->H, static_cast<const float*>(nullptr));
 }
 
-static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, bool fold, hipStream_t st) {
+static void launch_prep(const VissmFlowDesc* d, const VissmFlowParams* w, const Ws& ws, bool fold, hipStream_t st,
+                        bool lofold = false) {
   const int JB = jb_of(d->k), KB = (JB + 1) / 2;
   hipLaunchKernelGGL(prep_kernel, dim3(n_frags(d->n_hidden, KB, JB)), dim3(64), 0, st, *w, d->H, d->k, d->n_hidden,
-                     d->bn, np_of(d), KB, JB, ws.img, ws.cst, fold ? 1 : 0);
+                     d->bn, np_of(d), KB, JB, ws.img, ws.cst, fold ? 1 : 0, lofold ? 1 : 0);
 }
 
 int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w, const float* u, const float* C, const int32_t* win,
@@ -2985,7 +3106,8 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   Ws ws;
   ws_layout(d, g, false, reinterpret_cast<char*>(workspace), &ws);
   const bool f2 = fwd2_ok(d, g), fold = f2 && fold_ok(d, w);
-  launch_prep(d, w, ws, fold, st);
+  const bool lof = f2 && lofold_ok(d);
+  launch_prep(d, w, ws, fold, st, lof);
   launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
@@ -2998,22 +3120,27 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
 // block's weight image then serves twice the waves and the LDS no longer caps them at 2-3 per SIMD; the bf16 AR forward
 // keeps 4-wave blocks with register-resident hi planes (8-wave blocks: 6.90 -> 7.16 ms, still four waves per SIMD at
 // 103 VGPRs), profiles/r04/ab_fwd_blocks_steps.log
-#define FWD2_LAUNCH(TF_, NP_, NH_, JB_)                                                                            \
+#ifndef VISSM_X2_NWF
+#define VISSM_X2_NWF 4  // split-weight forward with lofold: 4-wave blocks, hi planes register-resident (8.38 -> 8.26 ms
+                        // per AR-cfg launch against 8-wave blocks reading every plane from LDS, profiles/r06/ab_r06e.log)
+#endif
+#define FWD2_LAUNCH(TF_, NP_, NH_, JB_, LOF_)                                                                      \
   do {                                                                                                           \
-    constexpr int nwf = (NP_ == 2 || NH_ == 3) ? 8 : NW;                                                           \
-    hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_, nwf>), dim3((g.n_items + nwf - 1) / nwf), dim3(64 * nwf), \
-                       0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, ws.ls_slab, ws.thf);                   \
+    constexpr int nwf = (NP_ == 2 && LOF_) ? VISSM_X2_NWF : (NP_ == 2 || NH_ == 3) ? 8 : NW;                      \
+    hipLaunchKernelGGL((fwd2_kernel<TF_, NP_, NH_, JB_, nwf, LOF_>), dim3((g.n_items + nwf - 1) / nwf),            \
+                       dim3(64 * nwf), 0, st, a, u, ws.Cp, ws.thp, ws.img, ws.cst, u_next, ws.ls_slab, ws.thf);   \
   } while (0)
     const int jb = jb_of(d->k);
     if (d->n_hidden == 3) {
-      if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1);
-      else if (jb == 2) FWD2_LAUNCH(false, 1, 3, 2);
-      else if (jb == 3) FWD2_LAUNCH(false, 1, 3, 3);
-      else FWD2_LAUNCH(false, 1, 3, 4);
+      if (jb == 1) FWD2_LAUNCH(false, 1, 3, 1, false);
+      else if (jb == 2) FWD2_LAUNCH(false, 1, 3, 2, false);
+      else if (jb == 3) FWD2_LAUNCH(false, 1, 3, 3, false);
+      else FWD2_LAUNCH(false, 1, 3, 4, false);
     }
-    else if (jb == 2) { if (np_of(d) == 2) FWD2_LAUNCH(false, 2, 1, 2); else FWD2_LAUNCH(false, 1, 1, 2); }
-    else if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2, 1, 1); else FWD2_LAUNCH(false, 2, 1, 1); }
-    else { if (fold) FWD2_LAUNCH(true, 1, 1, 1); else FWD2_LAUNCH(false, 1, 1, 1); }
+    else if (jb == 2) { if (np_of(d) == 2) FWD2_LAUNCH(false, 2, 1, 2, false); else FWD2_LAUNCH(false, 1, 1, 2, false); }
+    else if (np_of(d) == 2 && lof) { if (fold) FWD2_LAUNCH(true, 2, 1, 1, true); else FWD2_LAUNCH(false, 2, 1, 1, true); }
+    else if (np_of(d) == 2) { if (fold) FWD2_LAUNCH(true, 2, 1, 1, false); else FWD2_LAUNCH(false, 2, 1, 1, false); }
+    else { if (fold) FWD2_LAUNCH(true, 1, 1, 1, false); else FWD2_LAUNCH(false, 1, 1, 1, false); }
 #undef FWD2_LAUNCH
   } else if (np_of(d) == 2) {
     if (jb_of(d->k) == 1)
@@ -3039,7 +3166,7 @@ int VISSM_FLOW5_API(flow5_bwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
   Ws ws;
   ws_layout(d, g, true, reinterpret_cast<char*>(workspace), &ws);
   const bool b2 = !bwd2n_ok(d, g) && bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
-  launch_prep(d, w, ws, fold, st);
+  launch_prep(d, w, ws, fold, st, b2 && lofold_ok(d));
   launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_prep");
   KArgs a = make_args(d, g);
@@ -3152,7 +3279,7 @@ int VISSM_FLOW5_API(flow5_ar_fused)(const VissmFlowDesc* d, const VissmFlowParam
   VISSM_CHECK_ARG(!x2 || (g.S == S && d->n_win == 1 && d->k <= KP2),
                   "flow_ar_elbo_fused: bf16x2 needs the two-sample kernel's geometry (one window, k <= %d)", KP2);
   const bool b2 = x2 || bwd2_ok(d, g), fold = b2 && fold_ok(d, w);
-  launch_prep(d, w, ws, fold, st);
+  launch_prep(d, w, ws, fold, st, x2 && lofold_ok(d));
   launch_pad(d, w, g, C, theta_term, ws, fold, st);
   VISSM_CHECK_LAUNCH("flow5_fused_prep");
   KArgs a = make_args(d, g);
