@@ -39,6 +39,11 @@ constexpr int kSW = 4;  // trajectories (waves) per 256-thread block
 #ifndef VISSM_ELBO_ONEPASS_NB
 #define VISSM_ELBO_ONEPASS_NB 1   // vissm_elbo_fwd_grad's LV / SV / FHN kernel: neighbour exchange (0: chunk-local)
 #endif
+// waves per trajectory of that kernel by model (stream_onepass_kernel NWV).  One: two or four waves per trajectory
+// measured slower for every model (SV 51.8 -> 57.4 / 71.4 us, FHN 75.9 -> 80.6 / 91.4, LV 385 -> 405 / 443 us per
+// launch, profiles/r06/ab_r06i.log): the launch already fills the chip, and each range adds its edge states, transition
+// and the block barrier
+constexpr int kNwvLV = 1, kNwvSV = 1, kNwvFHN = 1;
 
 __device__ __forceinline__ f4u ld4(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 
@@ -644,7 +649,13 @@ __device__ __forceinline__ float lane_val(float v, int l) {
 
 // OL (VissmElboData.obs_list): the observation term leaves the chunk loop and the element-wise tail (no obs / obs_bin
 // row loads there) and is evaluated after them at the window's listed elements only, its dz added to the stored one.
-template <int MODEL, bool OL = false>
+// NWV > 1: NWV waves of the block share one trajectory, each taking a contiguous range of the chunk loop's iterations
+// (finer work units than one wave per trajectory: the launch's last round of waves no longer runs on a partly empty
+// chip).  A range starts from x of the element before it (one state evaluated) and ends by evaluating the transition
+// out of its deferred chunk's last element itself (its head; the transition is counted by the wave that owns it); the
+// last wave runs the element-wise tail; the per-sample sums are combined in wave order through LDS after a block
+// barrier (fixed order: deterministic).
+template <int MODEL, bool OL = false, int NWV = 1>
 __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float* __restrict__ z,
                                                              const float* __restrict__ theta,
                                                              const float* __restrict__ g_sde,
@@ -653,9 +664,16 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
                                                              float* __restrict__ dtheta, Vals vo) {
   using Dv = Dev<MODEL>;
   constexpr int ZD = Dv::ZD, P = Dv::P;
+  static_assert(!OL || NWV == 1, "the observation list's post-pass reads the whole row the wave wrote");
+  static_assert(kSW % NWV == 0, "whole trajectories per block");
   const int lane = threadIdx.x & 63;
-  const int b = __builtin_amdgcn_readfirstlane(blockIdx.x * kSW + (threadIdx.x >> 6));
-  if (b >= a.B) return;  // wave-uniform
+  const int wv = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) % NWV);  // this wave's range of the trajectory
+  const int b0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (kSW / NWV) + (threadIdx.x >> 6) / NWV);
+  // (NWV > 1: every wave reaches the block barrier below, so one past the batch evaluates the last trajectory and
+  //  stores nothing)
+  const bool live = b0 < a.B;
+  if (NWV == 1 && !live) return;  // wave-uniform
+  const int b = live ? b0 : a.B - 1;
   const int M = a.M;
   const int w = a.d.win ? a.d.win[b] : 0;
   Dv m;
@@ -707,6 +725,10 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     }
   };
   const int nfull = (M + 1) / kV;  // chunks whose kV elements all exist (elements 0 .. M)
+  // this wave's iterations of the chunk loop: [it_lo, it_hi) of nit (64 chunks each); the last wave runs the tail
+  const int nit = nfull >= 2 ? (nfull - 1 + 63) / 64 : 0;
+  const int it_lo = (nit * wv) / NWV, it_hi = (nit * (wv + 1)) / NWV;
+  const bool last_wave = wv == NWV - 1;
   // ---- the chunk loop: chunks 1 .. nfull - 1 ----
   float pend[ZD * kV];             // the deferred chunk (meaningful in lane pl only)
   float pg[2] = {0.f, 0.f}, pj[2] = {0.f, 0.f};  // its last element's state gradient (without the head) and d x / d z
@@ -714,8 +736,8 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
 #pragma unroll
   for (int i = 0; i < ZD * kV; ++i) pend[i] = 0.f;
   float xc0 = 0.f, xc1 = 0.f;      // x of element t0 - 1 for lane 0
-  if (nfull >= 2) {
-    const St s3 = m.state(zb, kV - 1);
+  if (it_lo < it_hi) {
+    const St s3 = m.state(zb, kV * (1 + 64 * it_lo) - 1);
     xc0 = s3.x[0];
     xc1 = s3.x[1];
   }
@@ -756,7 +778,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     // the previous iteration's deferred chunk: its head is this iteration's lane-0 first transition
     if (pl >= 0) {
       const float h0 = lane_val(tr[0].gh[0], 0), h1 = lane_val(tr[0].gh[1], 0);
-      if (lane == pl) {
+      if (lane == pl && (NWV == 1 || live)) {
         const float g[2] = {pg[0] + gs * h0, pg[1] + gs * h1};
         if constexpr (ZD == 2) {
           pend[ZD * (kV - 1)] += g[0] * pj[0];
@@ -792,7 +814,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
       }
       dz_of(st[j], g, true, FULL ? 1.f : on, o + ZD * j);
     }
-    if (act && lane != dl) {
+    if (act && lane != dl && (NWV == 1 || live)) {
 #pragma unroll
       for (int i = 0; i < ZD * kV; i += 4)
         *reinterpret_cast<f4u*>(dzb + ZD * t0 + i) = f4u{o[i], o[i + 1], o[i + 2], o[i + 3]};
@@ -820,7 +842,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
   const int pf = a.d.plain_from ? a.d.plain_from[w] : (1 << 30);   // first element of the plain span
   using T_ = std::true_type;
   using F_ = std::false_type;
-  for (int c0 = 1; c0 < nfull; c0 += 64) {
+  for (int c0 = 1 + 64 * it_lo; c0 < nfull && c0 < 1 + 64 * it_hi; c0 += 64) {
     const bool plain = (MODEL != VISSM_MODEL_FHN) && kV * c0 >= pf;   // the whole iteration lies in the plain span
     const bool full = c0 + 63 < nfull;
     if (plain) {
@@ -831,9 +853,26 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
       else iteration(c0, F_{}, F_{});
     }
   }
-  // ---- element-wise tail: elements [0, kV) and [kV nfull, M] ----
+  // a range other than the last: its deferred chunk's head is the transition out of its last element, which the next
+  // range counts (evaluated here by every lane at the same wave-uniform element, applied by the deferring lane)
+  if (NWV > 1 && !last_wave && pl >= 0) {
+    const em::TG h = m.trans(m.state(zb, pt0 + kV - 1), m.state(zb, pt0 + kV));
+    if (lane == pl && live) {
+      if constexpr (ZD == 2) {
+        pend[ZD * (kV - 1)] += (pg[0] + gs * h.gh[0]) * pj[0];
+        pend[ZD * (kV - 1) + 1] += (pg[1] + gs * h.gh[1]) * pj[1];
+      } else {
+        pend[kV - 1] += (pg[1] + gs * h.gh[1]) * pj[1];
+      }
+#pragma unroll
+      for (int i = 0; i < ZD * kV; i += 4)
+        *reinterpret_cast<f4u*>(dzb + ZD * pt0 + i) = f4u{pend[i], pend[i + 1], pend[i + 2], pend[i + 3]};
+    }
+    pl = -1;
+  }
+  // ---- element-wise tail: elements [0, kV) and [kV nfull, M] (the last wave) ----
   const int lo_end = nfull >= 1 ? kV : M + 1;
-  const int nrest = lo_end + (nfull >= 1 ? (M + 1 - kV * nfull) : 0);
+  const int nrest = last_wave ? lo_end + (nfull >= 1 ? (M + 1 - kV * nfull) : 0) : 0;
   float hpend0 = 0.f, hpend1 = 0.f;   // the head of element kV nfull - 1 (the deferred chunk's last element)
   for (int r0 = 0; r0 < nrest; r0 += 64) {
     const int r = r0 + lane;
@@ -862,7 +901,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
     }
     float o[ZD];
     dz_of(sc, g, on_r && t >= 1, on_r ? 1.f : 0.f, o);
-    if (on_r) {
+    if (on_r && (NWV == 1 || live)) {
       if constexpr (ZD == 2) {
         dzb[2 * t] = o[0];
         dzb[2 * t + 1] = o[1];
@@ -878,7 +917,7 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
       h0 = lane_val(hpend0, lo_end % 64);
       h1 = lane_val(hpend1, lo_end % 64);
     }
-    if (lane == pl) {
+    if (lane == pl && (NWV == 1 || live)) {
       if constexpr (ZD == 2) {
         pend[ZD * (kV - 1)] += (pg[0] + gs * h0) * pj[0];
         pend[ZD * (kV - 1) + 1] += (pg[1] + gs * h1) * pj[1];
@@ -912,15 +951,33 @@ __global__ __launch_bounds__(256) void stream_onepass_kernel(Args a, const float
       }
     }
   }
+  double r[P + 4];
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const double s = wave_sum(static_cast<double>(acc[i]));
-    if (lane == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(gs * s);
+  for (int i = 0; i < P; ++i) r[i] = wave_sum(static_cast<double>(acc[i]));
+  r[P] = wave_sum(static_cast<double>(s_lp));
+  r[P + 1] = wave_sum(static_cast<double>(s_q));
+  r[P + 2] = wave_sum(static_cast<double>(s_b));
+  r[P + 3] = wave_sum(static_cast<double>(s_e));
+  if constexpr (NWV > 1) {
+    // the ranges' sums in wave order (the trajectory's first wave writes)
+    __shared__ double part[kSW][P + 4];
+    const int wi = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < P + 4; ++i) part[wi][i] = r[i];
+    __syncthreads();
+    if (wv != 0 || !live) return;
+#pragma unroll
+    for (int i = 0; i < P + 4; ++i) {
+      double t = part[wi][i];
+      for (int v = 1; v < NWV; ++v) t += part[wi + v][i];
+      r[i] = t;
+    }
   }
-  const double r_lp = wave_sum(static_cast<double>(s_lp));
-  const double r_q = wave_sum(static_cast<double>(s_q));
-  const double r_b = wave_sum(static_cast<double>(s_b));
-  const double r_e = wave_sum(static_cast<double>(s_e));
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+    if (lane == 0) dtheta[static_cast<size_t>(b) * P + i] = static_cast<float>(gs * r[i]);
+  const double r_lp = r[P], r_q = r[P + 1], r_b = r[P + 2], r_e = r[P + 3];
   if (lane == 0) {
     vo.sde[b] = static_cast<float>(r_lp);
     if (vo.obs)
@@ -1257,6 +1314,21 @@ int vissm_elbo_bwd(const VissmElboDesc* d, const VissmElboData* data, const floa
   return VISSM_OK;
 }
 
+}  // extern "C"
+
+// waves per trajectory of vissm_elbo_fwd_grad's LV / SV / FHN kernel (stream_onepass_kernel's NWV): enough work units
+// for the launch to fill the chip in whole rounds; VISSM_ELBO_NWV = 1 / 2 / 4 overrides (A/B timing)
+static int onepass_waves(const VissmElboDesc* d) {
+  static const int env = [] {
+    const char* e = std::getenv("VISSM_ELBO_NWV");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env == 1 || env == 2 || env == 4) return env;
+  return d->model == VISSM_MODEL_LV ? kNwvLV : d->model == VISSM_MODEL_SV ? kNwvSV : kNwvFHN;
+}
+
+extern "C" {
+
 int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const float* z, const float* theta,
                         const float* g_sde, const float* g_obs, const float* g_extra, float* sde, float* obs,
                         float* extra, float* dz, float* dtheta, void* stream) {
@@ -1277,19 +1349,27 @@ int vissm_elbo_fwd_grad(const VissmElboDesc* d, const VissmElboData* data, const
                          g_obs, dz, dtheta, vo);
       break;
 #if VISSM_ELBO_ONEPASS_NB
+#define ONEPASS(MODEL_, OL_, NWV_)                                                                                  \
+  hipLaunchKernelGGL((stream_onepass_kernel<MODEL_, OL_, NWV_>), dim3((d->B * NWV_ + kSW - 1) / kSW), blk, 0, st, a, \
+                     z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo)
+#define ONEPASS_NWV(MODEL_)                                                                                       \
+  do {                                                                                                           \
+    const int nwv_ = onepass_waves(d);                                                                           \
+    if (nwv_ == 4) ONEPASS(MODEL_, false, 4);                                                                    \
+    else if (nwv_ == 2) ONEPASS(MODEL_, false, 2);                                                               \
+    else ONEPASS(MODEL_, false, 1);                                                                              \
+  } while (0)
     case VISSM_MODEL_LV:
-      if (ol)
-        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
-      else
-        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_LV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      if (ol) ONEPASS(VISSM_MODEL_LV, true, 1);
+      else ONEPASS_NWV(VISSM_MODEL_LV);
       break;
-    case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_SV>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
+    case VISSM_MODEL_SV: ONEPASS_NWV(VISSM_MODEL_SV); break;
     default:
-      if (ol)
-        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
-      else
-        hipLaunchKernelGGL((stream_onepass_kernel<VISSM_MODEL_FHN>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo);
+      if (ol) ONEPASS(VISSM_MODEL_FHN, true, 1);
+      else ONEPASS_NWV(VISSM_MODEL_FHN);
       break;
+#undef ONEPASS_NWV
+#undef ONEPASS
 #else
     case VISSM_MODEL_LV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_LV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;
     case VISSM_MODEL_SV: hipLaunchKernelGGL((stream_bwd_kernel<VISSM_MODEL_SV, true>), grid, blk, 0, st, a, z, theta, g_sde, g_obs, g_extra, dz, dtheta, vo); break;

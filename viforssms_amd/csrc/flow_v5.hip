@@ -3121,8 +3121,9 @@ int VISSM_FLOW5_API(flow5_fwd)(const VissmFlowDesc* d, const VissmFlowParams* w,
 // keeps 4-wave blocks with register-resident hi planes (8-wave blocks: 6.90 -> 7.16 ms, still four waves per SIMD at
 // 103 VGPRs), profiles/r04/ab_fwd_blocks_steps.log
 #ifndef VISSM_X2_NWF
-#define VISSM_X2_NWF 4  // split-weight forward with lofold: 4-wave blocks, hi planes register-resident (8.38 -> 8.26 ms
-                        // per AR-cfg launch against 8-wave blocks reading every plane from LDS, profiles/r06/ab_r06e.log)
+#define VISSM_X2_NWF 8  // split-weight forward with lofold: 8-wave blocks reading every plane from LDS (4-wave blocks with
+                        // the hi planes register-resident, 155 VGPRs: 8.47 -> 9.06 ms per AR-cfg launch,
+                        // profiles/r06/ab_r06i.log)
 #endif
 #define FWD2_LAUNCH(TF_, NP_, NH_, JB_, LOF_)                                                                      \
   do {                                                                                                           \
