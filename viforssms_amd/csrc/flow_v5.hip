@@ -367,6 +367,11 @@ __host__ __device__ __forceinline__ int fold_index(int kk, int R, int* which) {
 }
 __device__ __forceinline__ float bf16_hi(float x) { return static_cast<float>(static_cast<__bf16>(x)); }
 
+// the split-weight forward's 8-wave blocks keep the hidden layer's hi planes in registers (122 VGPRs, still four waves per
+// SIMD): 8.46 -> 8.39 ms per AR-cfg launch, profiles/r06/ab_r06j.log
+#ifndef VISSM_X2_HIDREG
+#define VISSM_X2_HIDREG 1
+#endif
 #ifndef VISSM_NO_LOFOLD
 #define VISSM_NO_LOFOLD 0  // (A/B switch: 1 keeps the separate lo MFMAs)
 #endif
@@ -2113,6 +2118,13 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
   constexpr bool HIREG = NWF == NW;
   constexpr int NWR = HIREG ? 8 * NH + 4 * KB + 2 : 1;
   bf8 wr[NWR];
+  // (VISSM_X2_HIDREG, 8-wave split-weight blocks with lofold: the hidden layer's hi planes register-resident)
+  constexpr bool HIDREG = !HIREG && LOF && VISSM_X2_HIDREG;
+  bf8 wrh[HIDREG ? 8 * NH : 1];
+  if constexpr (HIDREG) {
+#pragma unroll
+    for (int i = 0; i < 8 * NH; ++i) wrh[i] = sh.img[i][0][lane];
+  }
   if constexpr (HIREG) {
 #pragma unroll
     for (int i = 0; i < 8 * NH; ++i) wr[i] = sh.img[i][0][lane];
@@ -2125,6 +2137,7 @@ __global__ __launch_bounds__(64 * NWF, 2) void fwd2_kernel(KArgs a, const float*
   auto W = [&](int f, int i) -> Fr8<NP> {
     Fr8<NP> r;
     if constexpr (HIREG) r.h = wr[i];
+    else if (HIDREG && f < 8 * NH) r.h = wrh[HIDREG ? f : 0];
     else r.h = sh.img[f][0][lane];
     if constexpr (NP == 2) r.l = sh.img[f][1][lane];
     return r;
