@@ -353,6 +353,66 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
                    const float* dC, const VissmFeatGrads* g, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Lotka-Volterra's window-shared feature branch and first conv (lotka_volterra_partial.py:71-82): per window,
+ *   H3 = elu(elu(elu(h0 W0 + b0) W1 + b1) W2 + b2)              [R][H]   (R = the window's time-feature rows)
+ *   D  = elu(H3 W3 + b3)                                        [R][U]   (the time-mixing dense layer, transposed
+ *                                                                         by the reference so that U is the conv's
+ *                                                                         time axis and R its channels)
+ *   C[m][h] = conv_b[h] + sum_{j<k} sum_{r<R} D[r][s m + j] conv_w[j][1 + r][h]
+ * Replaces the four tf.layers.dense, the transpose and the feature part of tf.layers.conv1d with their gradients:
+ * the three small layers in fp32 (vissm_lv_mlp_*), the time-mixing layer and the conv as bf16 matrix-core GEMMs
+ * (vissm_gemm_bf16) on operands packed by vissm_lv_pack, the conv's diagonal sum and its transpose by
+ * vissm_lv_conv_diag[_bwd], the conv weight gradient back to [k][1 + R][H] by vissm_lv_conv_wscatter
+ * (viforssms_amd/lvfeat.py chains them).  mlp_fwd writes act [3][n_win][R][H] (fp32 layer outputs) and H3b
+ * [n_win][R][64] bf16 (H3, a ones column at H for W3b's bias row, zeros); mlp_bwd takes dH3 [n_win][R][ld] (columns
+ * < H) and writes the gradients of W0..W2, b0..b2 (the w[3] / b[3] / conv fields of the grads struct unused).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t n_win, R, Cin, H;
+  int64_t in_win_stride;
+} VissmLvFeatDesc;
+
+size_t vissm_lv_mlp_workspace_size(const VissmLvFeatDesc* d);
+int vissm_lv_mlp_fwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, float* act, void* H3b,
+                     void* stream);
+int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, const float* act,
+                     const float* dH3, int ld_dH3, const VissmFeatGrads* g, void* workspace, size_t ws_bytes,
+                     void* stream);
+/* W3b [64][ldw] bf16 (rows < H: w3 [H][U], row H: b3, zeros; columns >= U zero) and Wc [R][ldc] bf16
+ * (Wc[r][j H + h] = conv_w[j][1 + r][h], zero for columns >= k H) */
+int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
+                  int ldc, void* Wc, void* stream);
+/* C[m][h] = conv_b[h] + sum_{j<k} G[s m + j][j H + h], G [U][ldg] fp32, m < Lh */
+int vissm_lv_conv_diag(const float* G, int ldg, const float* conv_b, int H, int k, int stride, int Lh, float* C,
+                       void* stream);
+/* its transpose: dG[u][j H + h] = dC[(u - j) / s][h] where that is a position (bf16 [U][ldg], zero elsewhere), and
+ * dconv_b[h] = sum_m dC[m][h] */
+int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, float* dconv_b,
+                           void* stream);
+/* dconv_w[j][1 + r][h] = dWc[r][j H + h]; channel 0 (the flow kernel's w_eps) = 0 */
+int vissm_lv_conv_wscatter(const float* dWc, int ldc, int R, int k, int H, float* dconv_w, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * bf16 matrix-core GEMM: C[m][n] = sum_k A[m][k] B[k][n], fp32 accumulation (the LV feature branch's products).
+ * A: a_kmajor = 0: A[m][k] at A[m lda + k]; 1: at A[k lda + m].  B: b_kmajor = 0: B[k][n] at B[n ldb + k]; 1: at
+ * B[k ldb + n].  lda, ldb multiples of 8, A and B 16-byte aligned.  Epilogues: VISSM_GEMM_F32 (fp32 C[m ldc + n]),
+ * VISSM_GEMM_ELU_BF16 (bf16 elu(acc)), VISSM_GEMM_DELU_BF16 (bf16 acc * elu'(y), y = aux[m ldc + n] a bf16 ELU
+ * output: y < 0 ? y + 1 : 1).  split_k > 1 (fp32 epilogue, ldc == N): per-split partials in the workspace summed in
+ * split order (deterministic).
+ * ------------------------------------------------------------------------- */
+#define VISSM_GEMM_F32 0
+#define VISSM_GEMM_ELU_BF16 1
+#define VISSM_GEMM_DELU_BF16 2
+typedef struct {
+  int64_t M, N, K, lda, ldb, ldc;
+  int32_t a_kmajor, b_kmajor, epilogue, split_k;
+} VissmGemmDesc;
+
+size_t vissm_gemm_workspace_size(const VissmGemmDesc* d);
+int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* C, const void* aux, void* workspace,
+                    size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;
  * lotka_volterra_partial.py:366-386; SV_dense.py:304-328) from device-resident
  * padded channel tables (built once, AR.py:135-150), keyed by the step's window

@@ -75,6 +75,18 @@ class FeatGrads(ctypes.Structure):
     _fields_ = [("w", _c_void_p * 4), ("b", _c_void_p * 4), ("conv_w", _c_void_p), ("conv_b", _c_void_p)]
 
 
+class LvFeatDesc(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("n_win", "R", "Cin", "H")] + [("in_win_stride", _i64)]
+
+
+GEMM_F32, GEMM_ELU_BF16, GEMM_DELU_BF16 = 0, 1, 2
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = ([(n, _i64) for n in ("M", "N", "K", "lda", "ldb", "ldc")] +
+                [(n, _i32) for n in ("a_kmajor", "b_kmajor", "epilogue", "split_k")])
+
+
 THETA_MAX_P, THETA_MAX_BIJ = 5, 8
 
 
@@ -116,6 +128,20 @@ SIGNATURES = {
                               _c_void_p]),
     "vissm_feat_bwd": (_i32, [ctypes.POINTER(FeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p, _c_void_p,
                               ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_lv_mlp_workspace_size": (_size_t, [ctypes.POINTER(LvFeatDesc)]),
+    "vissm_lv_mlp_fwd": (_i32, [ctypes.POINTER(LvFeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p,
+                                _c_void_p, _c_void_p]),
+    "vissm_lv_mlp_bwd": (_i32, [ctypes.POINTER(LvFeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p,
+                                _c_void_p, _i32, ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
+    "vissm_lv_pack": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32,
+                             _c_void_p, _c_void_p]),
+    "vissm_lv_conv_diag": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vissm_lv_conv_diag_bwd": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p,
+                                      _c_void_p]),
+    "vissm_lv_conv_wscatter": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vissm_gemm_workspace_size": (_size_t, [ctypes.POINTER(GemmDesc)]),
+    "vissm_gemm_bf16": (_i32, [ctypes.POINTER(GemmDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                               _size_t, _c_void_p]),
     "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,

@@ -454,6 +454,207 @@ static Params params(const VissmFeatParams* w) {
   return p;
 }
 
+// ---------------------------------------------------------------------------
+// Lotka-Volterra's feature branch (lotka_volterra_partial.py:71-82): the first three dense + ELU layers over the
+// window's R time-feature rows, H3 = elu(elu(elu(h0 W0 + b0) W1 + b1) W2 + b2), here in fp32 (32 rows per block, the
+// dense_elu / wgrad code above); the time-mixing layer D = elu(H3 W3 + b3) ([R][U], U = the conv's time axis) and the
+// first conv over D's R channels are matrix-core GEMMs (vissm_gemm_bf16) on the operands packed below.
+// ---------------------------------------------------------------------------
+constexpr int kLvRows = 32;   // rows per block
+constexpr int kLvC = 64;      // columns of H3b: H3, then the ones column (W3b's bias row), then zeros
+
+struct LvArgs {
+  int n_win, R, Cin, H;
+  int64_t in_ws;   // floats between windows of h0
+};
+
+// slab row layout of the three layers' gradients: W0 [Cin][H], b0, W1 [H][H], b1, W2, b2
+__host__ __device__ inline int lv_off_w(int l, int Cin, int H) { return l == 0 ? 0 : Cin * H + H + (l - 1) * (H * H + H); }
+__host__ __device__ inline int lv_n(int Cin, int H) { return Cin * H + H + 2 * (H * H + H); }
+
+// forward: grid (ceil(R / 32), n_win); act [3][n_win][R][H] fp32 (the three layer outputs), H3b [n_win][R][64] bf16
+__global__ __launch_bounds__(kNT) void lv_mlp_fwd_kernel(LvArgs a, Params p, const float* __restrict__ h0,
+                                                         float* __restrict__ act, __bf16* __restrict__ H3b) {
+  const int H = a.H, hp = H + 1, ip = a.Cin + 1;
+  __shared__ float hA[kLvRows * 65], hB[kLvRows * 65], Ws[64 * 65];
+  const int w = blockIdx.y, r0 = blockIdx.x * kLvRows, nr = min(kLvRows, a.R - r0);
+  const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
+  for (int idx = threadIdx.x; idx < kLvRows * a.Cin; idx += kNT) {
+    const int r = idx / a.Cin, c = idx % a.Cin;
+    hA[r * ip + c] = r < nr ? src[idx] : 0.f;
+  }
+  stage_w(Ws, hp, p.w[0], a.Cin, H);
+  __syncthreads();
+  const size_t plane = static_cast<size_t>(a.n_win) * a.R * H;
+  float* ab = act + (static_cast<size_t>(w) * a.R + r0) * H;
+  dense_elu(hA, ip, a.Cin, Ws, hp, p.b[0], hB, hp, nr, H, ab, nr);
+  __syncthreads();
+  stage_w(Ws, hp, p.w[1], H, H);
+  __syncthreads();
+  dense_elu(hB, hp, H, Ws, hp, p.b[1], hA, hp, nr, H, ab + plane, nr);
+  __syncthreads();
+  stage_w(Ws, hp, p.w[2], H, H);
+  __syncthreads();
+  dense_elu(hA, hp, H, Ws, hp, p.b[2], hB, hp, nr, H, ab + 2 * plane, nr);
+  __syncthreads();
+  __bf16* ob = H3b + (static_cast<size_t>(w) * a.R + r0) * kLvC;
+  for (int idx = threadIdx.x; idx < nr * kLvC; idx += kNT) {
+    const int r = idx / kLvC, c = idx % kLvC;
+    ob[idx] = static_cast<__bf16>(c < H ? hB[r * hp + c] : (c == H ? 1.f : 0.f));
+  }
+}
+
+// backward: dH3 [n_win][R][ldd] fp32 (columns < H used) -> per-block partials of the three layers' gradients
+__global__ __launch_bounds__(kNT) void lv_mlp_bwd_kernel(LvArgs a, Params p, const float* __restrict__ h0,
+                                                         const float* __restrict__ act, const float* __restrict__ dH3,
+                                                         int ldd, float* __restrict__ slab) {
+  const int H = a.H, hp = H + 1, ip = a.Cin + 1;
+  __shared__ float Gc_[kLvRows * 65], Gn_[kLvRows * 65], Xs[kLvRows * 65], Ws[64 * 65];
+  float* Gc = Gc_;
+  float* Gn = Gn_;
+  const int w = blockIdx.y, b = blockIdx.x, r0 = b * kLvRows, nr = min(kLvRows, a.R - r0);
+  const size_t plane = static_cast<size_t>(a.n_win) * a.R * H;
+  float* out = slab + (static_cast<size_t>(w) * gridDim.x + b) * lv_n(a.Cin, H);
+  const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  // dz2 = dH3 * elu'(H3)
+  {
+    const float* X = act + 2 * plane + (static_cast<size_t>(w) * a.R + r0) * H;
+    const float* D = dH3 + (static_cast<size_t>(w) * a.R + r0) * ldd;
+    for (int idx = threadIdx.x; idx < kLvRows * hp; idx += kNT) {
+      const int r = idx / hp, c = idx % hp;
+      Gc[idx] = (r < nr && c < H) ? D[static_cast<size_t>(r) * ldd + c] * elu_d_out(X[static_cast<size_t>(r) * H + c]) : 0.f;
+    }
+  }
+  for (int l = 2; l >= 0; --l) {
+    const int nin = l == 0 ? a.Cin : H, xp = l == 0 ? ip : hp;
+    __syncthreads();
+    if (l == 0) {
+      const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
+      for (int idx = threadIdx.x; idx < kLvRows * a.Cin; idx += kNT) {
+        const int r = idx / a.Cin, c = idx % a.Cin;
+        Xs[r * ip + c] = r < nr ? src[idx] : 0.f;
+      }
+    } else {
+      const float* X = act + (l - 1) * plane + (static_cast<size_t>(w) * a.R + r0) * H;
+      for (int idx = threadIdx.x; idx < kLvRows * hp; idx += kNT) {
+        const int r = idx / hp, c = idx % hp;
+        Xs[idx] = (r < nr && c < H) ? X[static_cast<size_t>(r) * H + c] : 0.f;
+      }
+    }
+    if (l > 0) stage_w(Ws, hp, p.w[l], H, H);
+    __syncthreads();
+    const int ow = lv_off_w(l, a.Cin, H), obias = ow + nin * H;
+    wgrad(Xs, xp, nin, Gc, hp, nr, H, out + ow);
+    if (rg == 0 && o < H) {
+      float sb = 0.f;
+      for (int r = 0; r < nr; ++r) sb += Gc[r * hp + o];
+      out[obias + o] = sb;
+    }
+    if (l > 0) {
+      const int i = o;
+      if (i < H) {
+        for (int r0b = rg * 8; r0b < kLvRows; r0b += 32) {
+          float acc[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+          for (int oo = 0; oo < H; ++oo) {
+            const float wv = Ws[i * hp + oo];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = fmaf(Gc[(r0b + q) * hp + oo], wv, acc[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int r = r0b + q;
+            Gn[r * hp + i] = r < nr ? acc[q] * elu_d_out(Xs[r * hp + i]) : 0.f;
+          }
+        }
+      }
+      float* t = Gc;
+      Gc = Gn;
+      Gn = t;
+    }
+  }
+}
+
+__global__ void lv_mlp_scatter_kernel(const float* __restrict__ red, int Cin, int H, float* gw0, float* gb0,
+                                      float* gw1, float* gb1, float* gw2, float* gb2) {
+  float* gw[3] = {gw0, gw1, gw2};
+  float* gb[3] = {gb0, gb1, gb2};
+  const int n = lv_n(Cin, H);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int l = 2;
+    while (l > 0 && i < lv_off_w(l, Cin, H)) --l;
+    const int ow = lv_off_w(l, Cin, H), nin = l == 0 ? Cin : H;
+    if (i < ow + nin * H) gw[l][i - ow] = red[i];
+    else gb[l][i - ow - nin * H] = red[i];
+  }
+}
+
+// W3b [64][ldw] bf16: rows < H the time-mixing kernel W3 [H][U], row H its bias, the rest zero; Wc [R][ldc] bf16:
+// Wc[r][j H + h] = conv_w[j][1 + r][h] (the conv's feature channels), zero past k H
+__global__ void lv_pack_kernel(const float* __restrict__ w3, const float* __restrict__ b3, int H, int U, int ldw,
+                               __bf16* __restrict__ W3b, const float* __restrict__ cw, int R, int k, int ldc,
+                               __bf16* __restrict__ Wc) {
+  const int64_t n1 = static_cast<int64_t>(kLvC) * ldw, n2 = static_cast<int64_t>(R) * ldc;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n1 + n2;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    if (i < n1) {
+      const int c = static_cast<int>(i / ldw), u = static_cast<int>(i % ldw);
+      const float v = u >= U ? 0.f : c < H ? w3[static_cast<int64_t>(c) * U + u] : c == H ? b3[u] : 0.f;
+      W3b[i] = static_cast<__bf16>(v);
+    } else {
+      const int64_t e = i - n1;
+      const int r = static_cast<int>(e / ldc), n = static_cast<int>(e % ldc);
+      const int j = n / H, h = n % H;
+      Wc[e] = static_cast<__bf16>(j < k ? cw[(static_cast<int64_t>(j) * (1 + R) + 1 + r) * H + h] : 0.f);
+    }
+  }
+}
+
+// C[m][h] = conv_b[h] + sum_{j < k} G[s m + j][j H + h]  (G [U][ldg] fp32)
+__global__ void lv_diag_kernel(const float* __restrict__ G, int ldg, const float* __restrict__ cb, int H, int k,
+                               int s, int Lh, float* __restrict__ C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Lh * H) return;
+  const int m = i / H, h = i % H;
+  float v = cb[h];
+  for (int j = 0; j < k; ++j) v += G[static_cast<int64_t>(s * m + j) * ldg + j * H + h];
+  C[i] = v;
+}
+
+// dG[u][j H + h] = dC[(u - j) / s][h] where (u - j) / s is a position (bf16 [U][ldg], zero elsewhere and past k H):
+// grid (ceil(ldg / 256), U), 32-bit index arithmetic
+__global__ void lv_diag_bwd_kernel(const float* __restrict__ dC, int H, int k, int s, int Lh, int ldg,
+                                   __bf16* __restrict__ dG) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, u = blockIdx.y;
+  if (c >= ldg) return;
+  const int j = c / H, h = c - j * H, t = u - j;
+  float v = 0.f;
+  if (j < k && t >= 0 && t % s == 0 && t / s < Lh) v = dC[(t / s) * H + h];
+  dG[static_cast<int64_t>(u) * ldg + c] = static_cast<__bf16>(v);
+}
+
+// db[h] = sum_m dC[m][h]: one block per column, strided partial sums then the fixed-order block sum (deterministic)
+__global__ __launch_bounds__(256) void lv_colsum_kernel(const float* __restrict__ dC, int H, int Lh, float* __restrict__ db) {
+  __shared__ float red[4];
+  const int h = blockIdx.x;
+  float v = 0.f;
+  for (int m = threadIdx.x; m < Lh; m += 256) v += dC[static_cast<int64_t>(m) * H + h];
+  v = block_sum(v, red);
+  if (threadIdx.x == 0) db[h] = v;
+}
+
+// dconv_w[j][1 + r][h] = dWc[r][j H + h] (channel 0, the flow kernel's w_eps, gets zero)
+__global__ void lv_wscatter_kernel(const float* __restrict__ dWc, int ldc, int R, int k, int H, float* __restrict__ gcw) {
+  const int64_t n = static_cast<int64_t>(k) * (1 + R) * H;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < n;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int j = static_cast<int>(e / ((1 + R) * static_cast<int64_t>(H)));
+    const int c = static_cast<int>((e / H) % (1 + R)), h = static_cast<int>(e % H);
+    gcw[e] = c == 0 ? 0.f : dWc[static_cast<int64_t>(c - 1) * ldc + j * H + h];
+  }
+}
+
 }  // namespace feat
 }  // namespace vissm
 
@@ -528,6 +729,109 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
                      a.H, a.k, g->w[0], g->b[0], g->w[1], g->b[1], g->w[2], g->b[2], g->w[3], g->b[3], g->conv_w,
                      g->conv_b);
   VISSM_CHECK_LAUNCH("feat_scatter");
+  return VISSM_OK;
+}
+
+// ---- Lotka-Volterra's feature branch (the three fp32 layers and the GEMM operand packing; lotka_volterra_partial.py:71-82)
+static int lv_make(const VissmLvFeatDesc* d, feat::LvArgs* a) {
+  VISSM_CHECK_ARG(d && d->n_win >= 1 && d->R >= 1 && d->Cin >= 1 && d->Cin <= feat::kMaxCin && d->H >= 1 && d->H < feat::kLvC,
+                  "lv_feat: bad shape (Cin <= %d, H < %d)", feat::kMaxCin, feat::kLvC);
+  VISSM_CHECK_ARG(d->in_win_stride >= static_cast<int64_t>(d->R) * d->Cin || d->n_win == 1, "lv_feat: windows of h0 overlap");
+  a->n_win = d->n_win; a->R = d->R; a->Cin = d->Cin; a->H = d->H; a->in_ws = d->in_win_stride;
+  return VISSM_OK;
+}
+
+size_t vissm_lv_mlp_workspace_size(const VissmLvFeatDesc* d) {
+  feat::LvArgs a;
+  if (lv_make(d, &a)) return 0;
+  const int nb = (a.R + feat::kLvRows - 1) / feat::kLvRows;
+  const int n = feat::lv_n(a.Cin, a.H);
+  return align_up(static_cast<size_t>(a.n_win) * nb * n * sizeof(float)) + align_up(n * sizeof(float));
+}
+
+int vissm_lv_mlp_fwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, float* act, void* H3b,
+                     void* stream) {
+  feat::LvArgs a;
+  int rc = lv_make(d, &a);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && h0 && act && H3b, "lv_mlp_fwd: null pointer");
+  dim3 grid((a.R + feat::kLvRows - 1) / feat::kLvRows, a.n_win);
+  hipLaunchKernelGGL(feat::lv_mlp_fwd_kernel, grid, dim3(feat::kNT), 0, as_stream(stream), a, feat::params(w), h0, act,
+                     static_cast<__bf16*>(H3b));
+  VISSM_CHECK_LAUNCH("lv_mlp_fwd");
+  return VISSM_OK;
+}
+
+int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, const float* act,
+                     const float* dH3, int ld_dH3, const VissmFeatGrads* g, void* workspace, size_t ws_bytes,
+                     void* stream) {
+  feat::LvArgs a;
+  int rc = lv_make(d, &a);
+  if (rc) return rc;
+  VISSM_CHECK_ARG(w && h0 && act && dH3 && g && ld_dH3 >= d->H, "lv_mlp_bwd: bad argument");
+  VISSM_CHECK_ARG(workspace && ws_bytes >= vissm_lv_mlp_workspace_size(d), "lv_mlp_bwd: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int nb = (a.R + feat::kLvRows - 1) / feat::kLvRows;
+  const int n = feat::lv_n(a.Cin, a.H);
+  float* slab = static_cast<float*>(workspace);
+  float* red = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                        align_up(static_cast<size_t>(a.n_win) * nb * n * sizeof(float)));
+  hipLaunchKernelGGL(feat::lv_mlp_bwd_kernel, dim3(nb, a.n_win), dim3(feat::kNT), 0, st, a, feat::params(w), h0, act, dH3,
+                     ld_dH3, slab);
+  VISSM_CHECK_LAUNCH("lv_mlp_bwd");
+  rc = launch_reduce_rows(slab, red, static_cast<int64_t>(a.n_win) * nb, n, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(feat::lv_mlp_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, a.Cin, a.H, g->w[0],
+                     g->b[0], g->w[1], g->b[1], g->w[2], g->b[2]);
+  VISSM_CHECK_LAUNCH("lv_mlp_scatter");
+  return VISSM_OK;
+}
+
+int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
+                  int ldc, void* Wc, void* stream) {
+  VISSM_CHECK_ARG(w3 && b3 && W3b && conv_w && Wc && H >= 1 && H < feat::kLvC && U >= 1 && ldw >= U && R >= 1 &&
+                      k >= 1 && ldc >= k * H,
+                  "lv_pack: bad argument");
+  const int64_t n = static_cast<int64_t>(feat::kLvC) * ldw + static_cast<int64_t>(R) * ldc;
+  hipLaunchKernelGGL(feat::lv_pack_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 16384))),
+                     dim3(256), 0, as_stream(stream), w3, b3, H, U, ldw, static_cast<__bf16*>(W3b), conv_w, R, k, ldc,
+                     static_cast<__bf16*>(Wc));
+  VISSM_CHECK_LAUNCH("lv_pack");
+  return VISSM_OK;
+}
+
+int vissm_lv_conv_diag(const float* G, int ldg, const float* conv_b, int H, int k, int stride, int Lh, float* C,
+                       void* stream) {
+  VISSM_CHECK_ARG(G && conv_b && C && H >= 1 && k >= 1 && (stride == 1 || stride == 2) && Lh >= 1 && ldg >= k * H,
+                  "lv_conv_diag: bad argument");
+  hipLaunchKernelGGL(feat::lv_diag_kernel, dim3((Lh * H + 255) / 256), dim3(256), 0, as_stream(stream), G, ldg, conv_b,
+                     H, k, stride, Lh, C);
+  VISSM_CHECK_LAUNCH("lv_conv_diag");
+  return VISSM_OK;
+}
+
+int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, float* dconv_b,
+                           void* stream) {
+  VISSM_CHECK_ARG(dC && dG && dconv_b && H >= 1 && H <= 256 && k >= 1 && (stride == 1 || stride == 2) && Lh >= 1 &&
+                      ldg >= k * H && stride * (Lh - 1) + k <= U,
+                  "lv_conv_diag_bwd: bad argument");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(feat::lv_diag_bwd_kernel, dim3((ldg + 255) / 256, U), dim3(256), 0, st, dC, H, k, stride, Lh, ldg,
+                     static_cast<__bf16*>(dG));
+  VISSM_CHECK_LAUNCH("lv_conv_diag_bwd");
+  // the conv bias gradient: column sums of dC over its Lh rows (a single sequential pass per column was 0.65 ms of
+  // dependent loads at Lh = 5000)
+  hipLaunchKernelGGL(feat::lv_colsum_kernel, dim3(H), dim3(256), 0, st, dC, H, Lh, dconv_b);
+  VISSM_CHECK_LAUNCH("lv_conv_diag_bwd colsum");
+  return VISSM_OK;
+}
+
+int vissm_lv_conv_wscatter(const float* dWc, int ldc, int R, int k, int H, float* dconv_w, void* stream) {
+  VISSM_CHECK_ARG(dWc && dconv_w && R >= 1 && k >= 1 && H >= 1 && ldc >= k * H, "lv_conv_wscatter: bad argument");
+  const int64_t n = static_cast<int64_t>(k) * (1 + R) * H;
+  hipLaunchKernelGGL(feat::lv_wscatter_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 16384))),
+                     dim3(256), 0, as_stream(stream), dWc, ldc, R, k, H, dconv_w);
+  VISSM_CHECK_LAUNCH("lv_conv_wscatter");
   return VISSM_OK;
 }
 

@@ -1,0 +1,313 @@
+// Bf16 matrix-core GEMM with fused epilogues (vissm_gemm_bf16): C[m][n] = sum_k A[m][k] B[k][n], bf16 operands, fp32
+// accumulation, for the window-shared products of the Lotka-Volterra feature branch (lotka_volterra_partial.py:71-82:
+// the 50 -> kernel_ext - 1 time-mixing dense layer and the first conv over its 10,061 output channels, forward and
+// backward; lvfeat.hip), where the operands come in both orientations.
+//
+// Operand layouts (VissmGemmDesc): A row-major (a_kmajor = 0: A[m][k] at a[m lda + k], k contiguous) or K-major
+// (a_kmajor = 1: at a[k lda + m]); B "column-major" (b_kmajor = 0: B[k][n] at b[n ldb + k]) or K-major (b_kmajor = 1:
+// at b[k ldb + n]).  Rows are read in 16-byte chunks of 8 bf16 (leading dimensions multiples of 8, 16-byte aligned
+// pointers; chunks past the matrix edge read as zeros).
+//
+// Design: a 128 x 128 output tile per 256-thread block, 64 x 64 per wave (4 x 4 v_mfma_f32_16x16x32_bf16 blocks,
+// 64 accumulator registers); K in steps of 32 through two LDS buffers (global loads of step k + 1 in flight while step
+// k computes; one barrier per step).  An operand whose contiguous dimension is k sits in LDS as [row][k] with 80-byte
+// rows (fragment reads: two ds_read_b64 per lane, k = 4g..4g+3 and 16+4g..16+4g+3, conflict-free: the row stride is
+// 20 banks); a K-major one as [k][row] with 288-byte rows, read with ds_read_b64_tr_b16 (the same k order; row stride
+// 8 banks mod 64).  Epilogues: fp32 store, ELU -> bf16, x elu'(y) of a bf16 ELU output -> bf16.  Split-K
+// (gridDim.z > 1) writes per-split fp32 partials that a fixed-order pass sums (deterministic).
+#include "common.hpp"
+
+namespace vissm {
+namespace gemm {
+
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) bf4 lds_bf4;
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+constexpr int RP = BK + 8;     // [row][k] image pitch (elements): 80-byte rows
+constexpr int CP = 128 + 16;   // [k][row] image pitch: 288-byte rows
+constexpr int IMG = 128 * RP > BK * CP ? 128 * RP : BK * CP;   // elements per operand image
+
+struct KArgs {
+  int64_t M, N, K, lda, ldb, ldc;
+  int64_t kper;      // K range per split (multiple of BK)
+  int64_t slab;      // elements between split partials (split-K)
+};
+
+__device__ __forceinline__ f4 mfma32(bf8 a, bf8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ bf8 cat8(bf4 a, bf4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// 16-byte chunk (8 bf16) of a matrix whose rows of `ld` elements are contiguous: row r, columns c .. c + 7 (zeros past
+// the edge: r >= nr or c >= nc; nc is a multiple of 8 or the chunk is read element-wise)
+__device__ __forceinline__ u4v ld_chunk(const __bf16* __restrict__ p, int64_t ld, int64_t r, int64_t c, int64_t nr,
+                                        int64_t nc) {
+  if (r >= nr || c >= nc) return u4v{0u, 0u, 0u, 0u};
+  const __bf16* q = p + r * ld + c;
+  if (c + 8 <= nc) return *reinterpret_cast<const u4v*>(q);
+  bf8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = c + j < nc ? q[j] : static_cast<__bf16>(0.f);
+  return __builtin_bit_cast(u4v, v);
+}
+
+// the staging of one operand: two 16-byte chunks per thread per K-step
+//   KM = false: rows r0 .. r0 + 127 of a [rows][k] matrix (k contiguous): chunk q -> row q >> 2, k (q & 3) 8
+//   KM = true:  a [k][rows] matrix (rows contiguous): chunk q -> k q >> 4, row (q & 15) 8
+template <bool KM>
+struct Stage {
+  u4v v[2];
+  __device__ __forceinline__ void load(const __bf16* __restrict__ p, int64_t ld, int64_t r0, int64_t k0, int64_t nrows,
+                                       int64_t kend) {
+    if (r0 + 128 <= nrows && k0 + BK <= kend) {   // interior tile (block-uniform): no edge checks
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = threadIdx.x + NT * i;
+        if constexpr (!KM) v[i] = *reinterpret_cast<const u4v*>(p + (r0 + (q >> 2)) * ld + k0 + (q & 3) * 8);
+        else v[i] = *reinterpret_cast<const u4v*>(p + (k0 + (q >> 4)) * ld + r0 + (q & 15) * 8);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = threadIdx.x + NT * i;
+      if constexpr (!KM) v[i] = ld_chunk(p, ld, r0 + (q >> 2), k0 + (q & 3) * 8, nrows, kend);
+      else v[i] = ld_chunk(p, ld, k0 + (q >> 4), r0 + (q & 15) * 8, kend, nrows);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* img) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = threadIdx.x + NT * i;
+      if constexpr (!KM) *reinterpret_cast<u4v*>(img + (q >> 2) * RP + (q & 3) * 8) = v[i];
+      else *reinterpret_cast<u4v*>(img + (q >> 4) * CP + (q & 15) * 8) = v[i];
+    }
+  }
+};
+
+// K = 32 fragment of rows rb .. rb + 15 of the tile: lane (g, c) gets row rb + c, k = 4g + jj and 16 + 4g + jj
+template <bool KM>
+__device__ __forceinline__ bf8 frag(const __bf16* img, int rb, int g, int c) {
+  if constexpr (!KM) {
+    const __bf16* p = img + (rb + c) * RP + 4 * g;
+    return cat8(*reinterpret_cast<const bf4*>(p), *reinterpret_cast<const bf4*>(p + 16));
+  } else {
+    const __bf16* p = img + (4 * g + (c >> 2)) * CP + rb + 4 * (c & 3);
+    return cat8(__builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)p),
+                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)(p + 16 * CP)));
+  }
+}
+
+__device__ __forceinline__ float elu_acc(float x) { return x > 0.f ? x : expm1f(x); }
+
+// EPI: 0 fp32 store (split-K: partial z at C + z slab), 1 ELU -> bf16, 2 x elu'(aux) -> bf16 (aux: bf16 ELU output,
+// same layout as C)
+template <bool AKM, bool BKM, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                     void* __restrict__ Cv, const __bf16* __restrict__ aux) {
+  // the two operands' double buffers in one array (the bf16 epilogue stages its 4 x 8.5 KB through all of it)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4][IMG];
+  __bf16(*sa)[IMG] = smem;
+  __bf16(*sb)[IMG] = smem + 2;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int wm = w >> 1, wn = w & 1;
+  // XCD-aware tile order: the dispatcher deals a grid's blocks round-robin over the 8 XCDs (each with its own L2), so
+  // consecutive block ids land on different L2s; renumbering them so that each XCD runs a contiguous run of tiles (all
+  // n-tiles of an m-tile together) lets the n-tiles sharing an A tile read it through one L2 instead of eight
+  int mt, nt;
+  {
+    const int nbx = gridDim.x, total = gridDim.x * gridDim.y;
+    const int b = blockIdx.y * nbx + blockIdx.x, x = b & 7, i = b >> 3;
+    const int per = total >> 3, rem = total & 7;
+    const int t = x * per + min(x, rem) + i;
+    mt = t / nbx;
+    nt = t - mt * nbx;
+  }
+  const int64_t m0 = static_cast<int64_t>(mt) * BM, n0 = static_cast<int64_t>(nt) * BN;
+  const int64_t kb = static_cast<int64_t>(blockIdx.z) * a.kper;
+  const int64_t ke = min(a.K, kb + a.kper);
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  Stage<AKM> la;
+  Stage<BKM> lb;
+  const int nk = static_cast<int>((ke - kb + BK - 1) / BK);
+  if (nk > 0) {
+    la.load(A, a.lda, m0, kb, a.M, ke);
+    lb.load(B, a.ldb, n0, kb, a.N, ke);
+    la.store(sa[0]);
+    lb.store(sb[0]);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(A, a.lda, m0, kb + static_cast<int64_t>(kt + 1) * BK, a.M, ke);
+      lb.load(B, a.ldb, n0, kb + static_cast<int64_t>(kt + 1) * BK, a.N, ke);
+    }
+    bf8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag<AKM>(sa[cur], wm * 64 + 16 * i, g, c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM>(sb[cur], wn * 64 + 16 * j, g, c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+    if (more) {
+      la.store(sa[cur ^ 1]);
+      lb.store(sb[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+  // epilogue: lane (g, c) of block (i, j) holds C[m = base_m + 16 i + 4 g + r][n = base_n + 16 j + c]
+  if constexpr (EPI != 0) {
+    // bf16 outputs through LDS (the operand buffers are free after the loop's last barrier): each wave writes its
+    // 64 x 64 fp32 tile in two 32-row halves into its own [32][64 + 4] region, then stores 8 consecutive columns per
+    // lane (16-byte stores; the elu' epilogue reads its aux chunk the same way) instead of scattered 2-byte stores
+    static_assert(4 * 32 * 68 * 4 <= 4 * IMG * 2, "epilogue staging exceeds the operand buffers");
+    float* stg = reinterpret_cast<float*>(&smem[0][0]) + w * (32 * 68);   // 4 waves x 8.5 KB
+    const int64_t bm = m0 + wm * 64, bn = n0 + wn * 64;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) stg[(16 * ii + 4 * g + r) * 68 + 16 * j + c] = acc[2 * half + ii][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // lane l: rows (l >> 3) + 8 t (t = 0..3) of the half, columns 8 (l & 7) .. + 7
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int rr = (lane >> 3) + 8 * t, cc = 8 * (lane & 7);
+        const int64_t m = bm + 32 * half + rr, n = bn + cc;
+        if (m >= a.M || n >= a.N) continue;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = stg[rr * 68 + cc + e];
+        __bf16* dst = reinterpret_cast<__bf16*>(Cv) + m * a.ldc + n;
+        const bool full = n + 8 <= a.N && ((m * a.ldc + n) & 7) == 0;
+        bf8 o;
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = static_cast<__bf16>(elu_acc(x[e]));
+        } else {
+          bf8 y;
+          const __bf16* src = aux + m * a.ldc + n;
+          if (full) y = *reinterpret_cast<const bf8*>(src);
+          else
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = n + e < a.N ? src[e] : static_cast<__bf16>(0.f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float yv = static_cast<float>(y[e]);
+            o[e] = static_cast<__bf16>(yv < 0.f ? x[e] * (yv + 1.f) : x[e]);
+          }
+        }
+        if (full) *reinterpret_cast<bf8*>(dst) = o;
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.N) dst[e] = o[e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + 16 * j + c;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+        if (m >= a.M) continue;
+        const float x = acc[i][j][r];
+        if constexpr (EPI == 0) {
+          reinterpret_cast<float*>(Cv)[static_cast<int64_t>(blockIdx.z) * a.slab + m * a.ldc + n] = x;
+        } else if constexpr (EPI == 1) {
+          reinterpret_cast<__bf16*>(Cv)[m * a.ldc + n] = static_cast<__bf16>(elu_acc(x));
+        } else {
+          const float y = static_cast<float>(aux[m * a.ldc + n]);
+          reinterpret_cast<__bf16*>(Cv)[m * a.ldc + n] = static_cast<__bf16>(y < 0.f ? x * (y + 1.f) : x);
+        }
+      }
+    }
+}
+
+}  // namespace gemm
+}  // namespace vissm
+
+using namespace vissm;
+using namespace vissm::gemm;
+
+extern "C" {
+
+size_t vissm_gemm_workspace_size(const VissmGemmDesc* d) {
+  if (!d || d->split_k <= 1) return 0;
+  return align_up(static_cast<size_t>(d->split_k) * d->M * d->N * sizeof(float));
+}
+
+int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* C, const void* aux, void* workspace,
+                    size_t ws_bytes, void* stream) {
+  VISSM_CHECK_ARG(d && A && B && C, "gemm_bf16: null argument");
+  VISSM_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "gemm_bf16: negative size");
+  if (d->M == 0 || d->N == 0) return VISSM_OK;
+  VISSM_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm_bf16: leading dimensions must be multiples of 8");
+  VISSM_CHECK_ARG((reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0,
+                  "gemm_bf16: A and B must be 16-byte aligned");
+  VISSM_CHECK_ARG(d->lda >= (d->a_kmajor ? d->M : d->K) && d->ldb >= (d->b_kmajor ? d->N : d->K),
+                  "gemm_bf16: leading dimension below the row length");
+  VISSM_CHECK_ARG(d->ldc >= d->N, "gemm_bf16: ldc < N");
+  VISSM_CHECK_ARG(d->epilogue >= VISSM_GEMM_F32 && d->epilogue <= VISSM_GEMM_DELU_BF16, "gemm_bf16: epilogue");
+  VISSM_CHECK_ARG(d->epilogue != VISSM_GEMM_DELU_BF16 || aux, "gemm_bf16: the elu' epilogue needs aux");
+  const int split = d->split_k > 1 ? d->split_k : 1;
+  VISSM_CHECK_ARG(split == 1 || (d->epilogue == VISSM_GEMM_F32 && d->ldc == d->N),
+                  "gemm_bf16: split-K needs the fp32 epilogue and ldc == N");
+  VISSM_CHECK_ARG(split == 1 || (workspace && ws_bytes >= vissm_gemm_workspace_size(d)),
+                  "gemm_bf16: workspace too small");
+  hipStream_t st = as_stream(stream);
+  KArgs a;
+  a.M = d->M; a.N = d->N; a.K = d->K; a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+  a.kper = ((d->K + split - 1) / split + BK - 1) / BK * BK;
+  if (a.kper <= 0) a.kper = BK;
+  a.slab = d->M * d->N;
+  const int nz = static_cast<int>((d->K + a.kper - 1) / a.kper) > 0 ? static_cast<int>((d->K + a.kper - 1) / a.kper) : 1;
+  dim3 grid(static_cast<unsigned>((d->N + BN - 1) / BN), static_cast<unsigned>((d->M + BM - 1) / BM),
+            static_cast<unsigned>(split == 1 ? 1 : nz));
+  void* out = split == 1 ? C : workspace;
+  const __bf16* pa = static_cast<const __bf16*>(A);
+  const __bf16* pb = static_cast<const __bf16*>(B);
+  const __bf16* px = static_cast<const __bf16*>(aux);
+#define GEMM_EPI(AK, BKk)                                                                                      \
+  do {                                                                                                       \
+    if (d->epilogue == VISSM_GEMM_F32) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0>), grid, dim3(NT), 0, st, a, pa, pb, out, px); \
+    else if (d->epilogue == VISSM_GEMM_ELU_BF16) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 1>), grid, dim3(NT), 0, st, a, pa, pb, out, px); \
+    else hipLaunchKernelGGL((gemm_kernel<AK, BKk, 2>), grid, dim3(NT), 0, st, a, pa, pb, out, px);            \
+  } while (0)
+  if (d->a_kmajor) {
+    if (d->b_kmajor) GEMM_EPI(true, true);
+    else GEMM_EPI(true, false);
+  } else {
+    if (d->b_kmajor) GEMM_EPI(false, true);
+    else GEMM_EPI(false, false);
+  }
+#undef GEMM_EPI
+  VISSM_CHECK_LAUNCH("gemm_bf16");
+  if (split > 1) return launch_reduce_rows(static_cast<const float*>(workspace), static_cast<float*>(C), grid.z, d->M * d->N, st);
+  return VISSM_OK;
+}
+
+}  // extern "C"

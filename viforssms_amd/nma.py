@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
+from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, lv_feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
                   ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad,
                   elbo_values_grad, theta_branch_bwd, theta_branch_fwd)
 from .params import ParamStore, glorot_uniform
@@ -278,6 +278,13 @@ class IAF:
             return feat_conv(h0, s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
                              p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
                              p("conv/kernel"), p("conv/bias"))
+        # LV at the bf16 precision: the hand-written branch (ops.lv_feat_conv: vissm_lv_* + vissm_gemm_bf16), LV-cfg
+        # step 64.0 -> 62.1 ms against the torch form (profiles/r06/lvfeat/); VISSM_LV_FEAT=torch selects the latter
+        if f == "lv" and ts.is_cuda and gemm == "bf16" and os.environ.get("VISSM_LV_FEAT", "hip") != "torch":
+            p = self._p
+            return lv_feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"),
+                                p("feat1/bias"), p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"),
+                                p("feat3/bias"), p("conv/kernel"), p("conv/bias"))
         return self.conv_shared(self.features(ts), Lh, s, gemm=gemm)
 
     def theta_factors(self, theta: torch.Tensor):

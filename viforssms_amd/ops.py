@@ -278,6 +278,110 @@ def feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_
     return FeatConvFn.apply(h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
 
 
+# ---------------------------------------------------------------------------------------
+# bf16 matrix-core GEMM (vissm_gemm_bf16) and Lotka-Volterra's feature branch built on it (vissm_lv_*)
+# ---------------------------------------------------------------------------------------
+def gemm_bf16(M: int, N: int, K: int, A, lda: int, a_kmajor: bool, B, ldb: int, b_kmajor: bool, C, ldc: int,
+              epilogue: int = 0, aux=None, split_k: int = 1):
+    """C[m][n] = sum_k A[m][k] B[k][n] on bf16 operands (layouts: include/vissm.h VissmGemmDesc); C fp32 or, for the
+    ELU / elu' epilogues, bf16."""
+    lib = _lib.load()
+    d = _lib.GemmDesc(M, N, K, lda, ldb, ldc, int(a_kmajor), int(b_kmajor), epilogue, split_k)
+    nb = lib.vissm_gemm_workspace_size(ctypes.byref(d))
+    ws = _workspace(nb, C.device) if nb else None
+    check(lib.vissm_gemm_bf16(ctypes.byref(d), ptr(A), ptr(B), ptr(C), ptr(aux) if aux is not None else None,
+                              ptr(ws) if ws is not None else None, nb, _lib.stream_handle(C.device)), "vissm_gemm_bf16")
+
+
+def _r8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+class LvFeatConvFn(torch.autograd.Function):
+    """Lotka-Volterra's window-shared conv input C [n_win, Lh, H] (lotka_volterra_partial.py:71-82): the three dense +
+    ELU layers of the window's time features h0 [n_win, R, Cin] (fp32, vissm_lv_mlp_*), the time-mixing layer
+    D = elu(H3 W3 + b3) [R, U] and the conv over D's R channels (transposed by the reference, U its time axis) as bf16
+    matrix-core GEMMs (vissm_gemm_bf16: the layer with its ELU in the epilogue, then G = D^T Wc [U, k H] and the
+    conv's diagonal sum), and the backward the same way (dD with elu' in the epilogue, dWc = D dG, dW3 = H3^T dP and
+    dH3 = dP W3^T split over K).  The bf16 precision's arithmetic (the torch form: fp32 layers, linear_bf16 conv)
+    plus bf16 operands in the time-mixing layer; the gradient reaches the four dense layers and the conv kernel (its
+    sample channel 0 gets zero: the flow kernel's w_eps) and bias."""
+
+    @staticmethod
+    def forward(ctx, h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+        ws = (W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+        _require_gpu(*ws)
+        n_win, R, Cin = h0.shape
+        if h0.dtype != torch.float32 or h0.stride(2) != 1 or h0.stride(1) != Cin:
+            h0 = h0.contiguous()
+        _require_gpu(h0)
+        H, U, k = W0.shape[1], W3.shape[1], conv_w.shape[0]
+        if tuple(conv_w.shape) != (k, 1 + R, H) or s * (Lh - 1) + k > U or H >= 64:
+            raise _lib.VissmError(f"lv_feat: conv_w {tuple(conv_w.shape)}, R {R}, U {U}, Lh {Lh}, s {s}: shapes "
+                                  "do not match")
+        dev = h0.device
+        Up, NC = _r8(U), _r8(k * H)
+        lib, st = _lib.load(), _lib.stream_handle(dev)
+        d = _lib.LvFeatDesc(n_win, R, Cin, H, h0.stride(0) if n_win > 1 else R * Cin)
+        p = _feat_params(ws)
+        act = torch.empty(3, n_win, R, H, dtype=torch.float32, device=dev)
+        H3b = torch.empty(n_win, R, 64, dtype=torch.bfloat16, device=dev)
+        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(act), ptr(H3b), st), "vissm_lv_mlp_fwd")
+        W3b = torch.empty(64, Up, dtype=torch.bfloat16, device=dev)
+        Wc = torch.empty(R, NC, dtype=torch.bfloat16, device=dev)
+        check(lib.vissm_lv_pack(ptr(W3), ptr(b3), H, U, Up, ptr(W3b), ptr(conv_w), R, k, NC, ptr(Wc), st),
+              "vissm_lv_pack")
+        D = torch.empty(n_win, R, Up, dtype=torch.bfloat16, device=dev)
+        G = torch.empty(U, NC, dtype=torch.float32, device=dev)
+        C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=dev)
+        for w in range(n_win):
+            gemm_bf16(R, U, 64, H3b[w], 64, False, W3b, Up, True, D[w], Up, _lib.GEMM_ELU_BF16)
+            gemm_bf16(U, NC, R, D[w], Up, True, Wc, NC, True, G, NC, _lib.GEMM_F32)
+            check(lib.vissm_lv_conv_diag(ptr(G), NC, ptr(conv_b), H, k, s, Lh, ptr(C[w]), st), "vissm_lv_conv_diag")
+        ctx.save_for_backward(h0, act, H3b, D, W3b, Wc, *ws)
+        ctx.dims = (d, n_win, R, H, U, k, s, Lh, Up, NC)
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        h0, act, H3b, D, W3b, Wc, *ws = ctx.saved_tensors
+        d, n_win, R, H, U, k, s, Lh, Up, NC = ctx.dims
+        dev = dC.device
+        dC = dC.contiguous()
+        lib, st = _lib.load(), _lib.stream_handle(dev)
+        dG = torch.empty(U, NC, dtype=torch.bfloat16, device=dev)
+        dP = torch.empty(R, Up, dtype=torch.bfloat16, device=dev)
+        dWc = torch.empty(n_win, R, NC, dtype=torch.float32, device=dev)
+        dW3b = torch.empty(n_win, 64, U, dtype=torch.float32, device=dev)
+        dH3 = torch.empty(n_win, R, 64, dtype=torch.float32, device=dev)
+        dcb = torch.empty(n_win, H, dtype=torch.float32, device=dev)
+        for w in range(n_win):
+            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG), ptr(dcb[w]), st),
+                  "vissm_lv_conv_diag_bwd")
+            gemm_bf16(R, U, NC, Wc, NC, False, dG, NC, False, dP, Up, _lib.GEMM_DELU_BF16, aux=D[w])
+            gemm_bf16(R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, _lib.GEMM_F32)
+            gemm_bf16(64, U, R, H3b[w], 64, True, dP, Up, True, dW3b[w], U, _lib.GEMM_F32, split_k=4)
+            gemm_bf16(R, 64, U, dP, Up, False, W3b, Up, False, dH3[w], 64, _lib.GEMM_F32, split_k=4)
+        if n_win > 1:   # (the reference's LV windows: one per step at the benchmark shapes)
+            dWc, dW3b, dcb = dWc.sum(0, keepdim=True), dW3b.sum(0, keepdim=True), dcb.sum(0, keepdim=True)
+        gr = [torch.empty_like(t) for t in ws[:6]]
+        dconv_w = torch.empty_like(ws[8])
+        check(lib.vissm_lv_conv_wscatter(ptr(dWc[0]), NC, R, k, H, ptr(dconv_w), st), "vissm_lv_conv_wscatter")
+        g = _lib.FeatGrads((ctypes.c_void_p * 4)(ptr(gr[0]), ptr(gr[2]), ptr(gr[4]), None),
+                           (ctypes.c_void_p * 4)(ptr(gr[1]), ptr(gr[3]), ptr(gr[5]), None), None, None)
+        nb = lib.vissm_lv_mlp_workspace_size(ctypes.byref(d))
+        if nb == 0:
+            raise _lib.VissmError(f"vissm_lv_mlp_workspace_size failed: {lib.vissm_last_error().decode()}")
+        wsb = _workspace(nb, dev)
+        check(lib.vissm_lv_mlp_bwd(ctypes.byref(d), ctypes.byref(_feat_params(ws)), ptr(h0), ptr(act), ptr(dH3), 64,
+                                   ctypes.byref(g), ptr(wsb), nb, st), "vissm_lv_mlp_bwd")
+        return (None, None, None, *gr, dW3b[0, :H], dW3b[0, H], dconv_w, dcb[0])
+
+
+def lv_feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+    return LvFeatConvFn.apply(h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+
+
 class MAFlowFn(torch.autograd.Function):
     """One IAF flow (IAF._create_flow, AR.py:50-85) -> (u_next, logsig)."""
 
