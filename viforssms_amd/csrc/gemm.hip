@@ -27,8 +27,16 @@ typedef unsigned u4v __attribute__((ext_vector_type(4)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) bf4 lds_bf4;
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-constexpr int RP = BK + 8;     // [row][k] image pitch (elements): 80-byte rows
+// K step: 32 (64 halves the barriers but takes 180 VGPRs and 72 KB of LDS, two blocks per CU instead of three: LV-cfg
+// step 61.75 -> 62.75 ms, profiles/r06/lvfeat/ab_bk64.log)
+#ifndef VISSM_GEMM_BK
+#define VISSM_GEMM_BK 32
+#endif
+constexpr int BM = 128, BN = 128, BK = VISSM_GEMM_BK, NT = 256;
+constexpr int KS = BK / 32;    // MFMA k-steps per K-step
+constexpr int CPR = BK / 8;    // 16-byte chunks per [row][k] image row
+constexpr int NCH = 128 * BK / 8 / NT;   // staged chunks per thread per operand
+constexpr int RP = BK + 8;     // [row][k] image pitch (elements): 80- or 144-byte rows (20 / 36 banks: conflict-free)
 constexpr int CP = 128 + 16;   // [k][row] image pitch: 288-byte rows
 constexpr int IMG = 128 * RP > BK * CP ? 128 * RP : BK * CP;   // elements per operand image
 
@@ -59,30 +67,30 @@ __device__ __forceinline__ u4v ld_chunk(const __bf16* __restrict__ p, int64_t ld
 //   KM = true:  a [k][rows] matrix (rows contiguous): chunk q -> k q >> 4, row (q & 15) 8
 template <bool KM>
 struct Stage {
-  u4v v[2];
+  u4v v[NCH];
   __device__ __forceinline__ void load(const __bf16* __restrict__ p, int64_t ld, int64_t r0, int64_t k0, int64_t nrows,
                                        int64_t kend) {
     if (r0 + 128 <= nrows && k0 + BK <= kend) {   // interior tile (block-uniform): no edge checks
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NCH; ++i) {
         const int q = threadIdx.x + NT * i;
-        if constexpr (!KM) v[i] = *reinterpret_cast<const u4v*>(p + (r0 + (q >> 2)) * ld + k0 + (q & 3) * 8);
+        if constexpr (!KM) v[i] = *reinterpret_cast<const u4v*>(p + (r0 + q / CPR) * ld + k0 + (q % CPR) * 8);
         else v[i] = *reinterpret_cast<const u4v*>(p + (k0 + (q >> 4)) * ld + r0 + (q & 15) * 8);
       }
       return;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int q = threadIdx.x + NT * i;
-      if constexpr (!KM) v[i] = ld_chunk(p, ld, r0 + (q >> 2), k0 + (q & 3) * 8, nrows, kend);
+      if constexpr (!KM) v[i] = ld_chunk(p, ld, r0 + q / CPR, k0 + (q % CPR) * 8, nrows, kend);
       else v[i] = ld_chunk(p, ld, k0 + (q >> 4), r0 + (q & 15) * 8, kend, nrows);
     }
   }
   __device__ __forceinline__ void store(__bf16* img) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int q = threadIdx.x + NT * i;
-      if constexpr (!KM) *reinterpret_cast<u4v*>(img + (q >> 2) * RP + (q & 3) * 8) = v[i];
+      if constexpr (!KM) *reinterpret_cast<u4v*>(img + (q / CPR) * RP + (q % CPR) * 8) = v[i];
       else *reinterpret_cast<u4v*>(img + (q >> 4) * CP + (q & 15) * 8) = v[i];
     }
   }
@@ -90,12 +98,12 @@ struct Stage {
 
 // K = 32 fragment of rows rb .. rb + 15 of the tile: lane (g, c) gets row rb + c, k = 4g + jj and 16 + 4g + jj
 template <bool KM>
-__device__ __forceinline__ bf8 frag(const __bf16* img, int rb, int g, int c) {
+__device__ __forceinline__ bf8 frag(const __bf16* img, int rb, int g, int c, int ks = 0) {
   if constexpr (!KM) {
-    const __bf16* p = img + (rb + c) * RP + 4 * g;
+    const __bf16* p = img + (rb + c) * RP + 32 * ks + 4 * g;
     return cat8(*reinterpret_cast<const bf4*>(p), *reinterpret_cast<const bf4*>(p + 16));
   } else {
-    const __bf16* p = img + (4 * g + (c >> 2)) * CP + rb + 4 * (c & 3);
+    const __bf16* p = img + (32 * ks + 4 * g + (c >> 2)) * CP + rb + 4 * (c & 3);
     return cat8(__builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)p),
                 __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf4*)(p + 16 * CP)));
   }
@@ -151,15 +159,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
       la.load(A, a.lda, m0, kb + static_cast<int64_t>(kt + 1) * BK, a.M, ke);
       lb.load(B, a.ldb, n0, kb + static_cast<int64_t>(kt + 1) * BK, a.N, ke);
     }
-    bf8 af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = frag<AKM>(sa[cur], wm * 64 + 16 * i, g, c);
+    for (int ks = 0; ks < KS; ++ks) {
+      bf8 af[4], bfr[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM>(sb[cur], wn * 64 + 16 * j, g, c);
+      for (int i = 0; i < 4; ++i) af[i] = frag<AKM>(sa[cur], wm * 64 + 16 * i, g, c, ks);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKM>(sb[cur], wn * 64 + 16 * j, g, c, ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+    }
     if (more) {
       la.store(sa[cur ^ 1]);
       lb.store(sb[cur ^ 1]);
