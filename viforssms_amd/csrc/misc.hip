@@ -171,6 +171,12 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
 }
 
 // two columns per thread (one 4-byte load of a bf16 pair per row), eight rows in flight, row order
+// rows in flight per thread of the bf16 slab reduction: 32 (AR-cfg dC reduce 0.389 -> 0.360 ms per launch against 8,
+// profiles/r06/ab_r06m.log; the sums stay in row order, bit-exact with the sequential fp32 sum)
+#ifndef VISSM_REDUCE_DEPTH
+#define VISSM_REDUCE_DEPTH 32
+#endif
+constexpr int kRedDepth = VISSM_REDUCE_DEPTH;
 __global__ __launch_bounds__(256) void reduce_rows_bf16_kernel(const __bf16* __restrict__ slab, float* __restrict__ out,
                                                                int64_t R, int64_t N) {
   const int64_t c = 2 * (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x);
@@ -181,6 +187,17 @@ __global__ __launch_bounds__(256) void reduce_rows_bf16_kernel(const __bf16* __r
     const bf2v* p = reinterpret_cast<const bf2v*>(slab + c);
     const int64_t st = N / 2;
     int64_t r = 0;
+    // VISSM_REDUCE_DEPTH rows in flight per thread (the launch has only ~8 waves per CU); the sums stay in row order
+    for (; r + kRedDepth <= R; r += kRedDepth) {
+      bf2v v[kRedDepth];
+#pragma unroll
+      for (int i = 0; i < kRedDepth; ++i) v[i] = p[(r + i) * st];
+#pragma unroll
+      for (int i = 0; i < kRedDepth; ++i) {
+        s0 += static_cast<float>(v[i][0]);
+        s1 += static_cast<float>(v[i][1]);
+      }
+    }
     for (; r + 8 <= R; r += 8) {
       bf2v v[8];
 #pragma unroll
