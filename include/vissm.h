@@ -363,32 +363,43 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
  * the three small layers in fp32 (vissm_lv_mlp_*), the time-mixing layer and the conv as bf16 matrix-core GEMMs
  * (vissm_gemm_bf16) on operands packed by vissm_lv_pack, the conv's diagonal sum and its transpose by
  * vissm_lv_conv_diag[_bwd], the conv weight gradient back to [k][1 + R][H] by vissm_lv_conv_wscatter
- * (viforssms_amd/lvfeat.py chains them).  mlp_fwd writes act [3][n_win][R][H] (fp32 layer outputs) and H3b
- * [n_win][R][64] bf16 (H3, a ones column at H for W3b's bias row, zeros); mlp_bwd takes dH3 [n_win][R][ld] (columns
- * < H) and writes the gradients of W0..W2, b0..b2 (the w[3] / b[3] / conv fields of the grads struct unused).
+ * (viforssms_amd/ops.py LvFeatConvFn chains them).  mlp_fwd writes act [n_layers][n_win][R][H] (fp32 layer outputs)
+ * and H3b [n_win][R][64] bf16 (the last layer's output, a ones column at H for W3b's bias row, zeros; H3lo, when not
+ * null, the same layout holding the bf16 residual of each element, hi + lo = the fp32 value to ~2^-16); mlp_bwd
+ * takes dH3 [n_win][R][ld] (columns < H) and writes the gradients of W0.., b0.. (the conv fields of the grads struct
+ * unused).
+ *
+ * Stochastic volatility's branch (SV_dense.py:50-62: four dense + ELU layers over the window's features with their
+ * first differences, then the conv over the 50 feature channels at k = 50) runs through the same entry points:
+ * n_layers = 4, sv_diff = 1 (h0 is then the window's time features [L][Cr] and row r of the MLP input is
+ * [h0[r + 1][0 .. Cr), h0[r + 1][c] - h0[r][c] for c < Cr - 2], so Cin = 2 Cr - 2 and R = L - 1), the conv as a
+ * split-bf16 GEMM (vissm_gemm_bf16x3) on F = H3b / H3lo and the packed conv kernel (vissm_lv_pack with ldw = 0).
  * ------------------------------------------------------------------------- */
 typedef struct {
   int32_t n_win, R, Cin, H;
   int64_t in_win_stride;
+  int32_t n_layers;   /* dense + ELU layers in the MLP: 0 or 3 (LV), 4 (SV) */
+  int32_t sv_diff;    /* 1: SV's first-difference input assembly (above) */
 } VissmLvFeatDesc;
 
 size_t vissm_lv_mlp_workspace_size(const VissmLvFeatDesc* d);
 int vissm_lv_mlp_fwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, float* act, void* H3b,
-                     void* stream);
+                     void* H3lo, void* stream);
 int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, const float* act,
                      const float* dH3, int ld_dH3, const VissmFeatGrads* g, void* workspace, size_t ws_bytes,
                      void* stream);
-/* W3b [64][ldw] bf16 (rows < H: w3 [H][U], row H: b3, zeros; columns >= U zero) and Wc [R][ldc] bf16
- * (Wc[r][j H + h] = conv_w[j][1 + r][h], zero for columns >= k H) */
+/* W3b [64][ldw] bf16 (rows < H: w3 [H][U], row H: b3, zeros; columns >= U zero; ldw = 0: none, w3 / b3 / W3b
+ * unused) and Wc [R][ldc] bf16 (Wc[r][j H + h] = conv_w[j][1 + r][h], zero for columns >= k H; Wc_lo, when not null,
+ * its bf16 residual plane) */
 int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
-                  int ldc, void* Wc, void* stream);
+                  int ldc, void* Wc, void* Wc_lo, void* stream);
 /* C[m][h] = conv_b[h] + sum_{j<k} G[s m + j][j H + h], G [U][ldg] fp32, m < Lh */
 int vissm_lv_conv_diag(const float* G, int ldg, const float* conv_b, int H, int k, int stride, int Lh, float* C,
                        void* stream);
-/* its transpose: dG[u][j H + h] = dC[(u - j) / s][h] where that is a position (bf16 [U][ldg], zero elsewhere), and
- * dconv_b[h] = sum_m dC[m][h] */
-int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, float* dconv_b,
-                           void* stream);
+/* its transpose: dG[u][j H + h] = dC[(u - j) / s][h] where that is a position (bf16 [U][ldg], zero elsewhere; dG_lo,
+ * when not null, the bf16 residual plane), and dconv_b[h] = sum_m dC[m][h] */
+int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, void* dG_lo,
+                           float* dconv_b, void* stream);
 /* dconv_w[j][1 + r][h] = dWc[r][j H + h]; channel 0 (the flow kernel's w_eps) = 0 */
 int vissm_lv_conv_wscatter(const float* dWc, int ldc, int R, int k, int H, float* dconv_w, void* stream);
 
@@ -411,6 +422,12 @@ typedef struct {
 size_t vissm_gemm_workspace_size(const VissmGemmDesc* d);
 int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* C, const void* aux, void* workspace,
                     size_t ws_bytes, void* stream);
+/* The split-bf16 form (fp32-class products: the operands' hi / lo bf16 planes, x = hi + lo to ~2^-16, the same
+ * layouts): C = A_hi B_hi + A_hi B_lo + A_lo B_hi, one launch whose K loop runs the three passes (split-K divides
+ * the 3 K range).  The fp32 epilogue only. */
+size_t vissm_gemm_bf16x3_workspace_size(const VissmGemmDesc* d);
+int vissm_gemm_bf16x3(const VissmGemmDesc* d, const void* A_hi, const void* A_lo, const void* B_hi, const void* B_lo,
+                      void* C, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;

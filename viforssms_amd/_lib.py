@@ -76,7 +76,8 @@ class FeatGrads(ctypes.Structure):
 
 
 class LvFeatDesc(ctypes.Structure):
-    _fields_ = [(n, _i32) for n in ("n_win", "R", "Cin", "H")] + [("in_win_stride", _i64)]
+    _fields_ = ([(n, _i32) for n in ("n_win", "R", "Cin", "H")] + [("in_win_stride", _i64)] +
+                [("n_layers", _i32), ("sv_diff", _i32)])
 
 
 GEMM_F32, GEMM_ELU_BF16, GEMM_DELU_BF16 = 0, 1, 2
@@ -130,18 +131,20 @@ SIGNATURES = {
                               ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
     "vissm_lv_mlp_workspace_size": (_size_t, [ctypes.POINTER(LvFeatDesc)]),
     "vissm_lv_mlp_fwd": (_i32, [ctypes.POINTER(LvFeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p,
-                                _c_void_p, _c_void_p]),
+                                _c_void_p, _c_void_p, _c_void_p]),
     "vissm_lv_mlp_bwd": (_i32, [ctypes.POINTER(LvFeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p,
                                 _c_void_p, _i32, ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
     "vissm_lv_pack": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32,
-                             _c_void_p, _c_void_p]),
+                             _c_void_p, _c_void_p, _c_void_p]),
     "vissm_lv_conv_diag": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vissm_lv_conv_diag_bwd": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p,
-                                      _c_void_p]),
+                                      _c_void_p, _c_void_p]),
     "vissm_lv_conv_wscatter": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vissm_gemm_workspace_size": (_size_t, [ctypes.POINTER(GemmDesc)]),
     "vissm_gemm_bf16": (_i32, [ctypes.POINTER(GemmDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                _size_t, _c_void_p]),
+    "vissm_gemm_bf16x3_workspace_size": (_size_t, [ctypes.POINTER(GemmDesc)]),
+    "vissm_gemm_bf16x3": (_i32, [ctypes.POINTER(GemmDesc)] + [_c_void_p] * 6 + [_size_t, _c_void_p]),
     "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,

@@ -466,41 +466,64 @@ constexpr int kLvC = 64;      // columns of H3b: H3, then the ones column (W3b's
 struct LvArgs {
   int n_win, R, Cin, H;
   int64_t in_ws;   // floats between windows of h0
+  int nl;          // dense + ELU layers (LV 3, SV 4)
+  int diff;        // SV's first-difference input (SV_dense.py:53)
 };
 
-// slab row layout of the three layers' gradients: W0 [Cin][H], b0, W1 [H][H], b1, W2, b2
+// slab row layout of the layers' gradients: W0 [Cin][H], b0, W1 [H][H], b1, ...
 __host__ __device__ inline int lv_off_w(int l, int Cin, int H) { return l == 0 ? 0 : Cin * H + H + (l - 1) * (H * H + H); }
-__host__ __device__ inline int lv_n(int Cin, int H) { return Cin * H + H + 2 * (H * H + H); }
+__host__ __device__ inline int lv_n(int Cin, int H, int nl) { return Cin * H + H + (nl - 1) * (H * H + H); }
 
-// forward: grid (ceil(R / 32), n_win); act [3][n_win][R][H] fp32 (the three layer outputs), H3b [n_win][R][64] bf16
+// the MLP input rows r0 .. r0 + nr - 1 of window w into X [32][ip] (zero rows past nr): h0's rows, or SV's
+// [x[r + 1][0 .. Cr), x[r + 1][c] - x[r][c] for c < Cr - 2] of the window's time features x [L][Cr], Cr = (Cin + 2) / 2
+__device__ inline void lv_load_in(float* X, int ip, const LvArgs& a, const float* __restrict__ h0, int w, int r0, int nr) {
+  const float* hw = h0 + static_cast<int64_t>(w) * a.in_ws;
+  const int Cr = (a.Cin + 2) / 2;
+  for (int idx = threadIdx.x; idx < kLvRows * a.Cin; idx += kNT) {
+    const int r = idx / a.Cin, c = idx % a.Cin;
+    float v = 0.f;
+    if (r < nr) {
+      if (!a.diff) {
+        v = hw[static_cast<int64_t>(r0 + r) * a.Cin + c];
+      } else {
+        const float* x1 = hw + static_cast<int64_t>(r0 + r + 1) * Cr;
+        v = c < Cr ? x1[c] : x1[c - Cr] - x1[c - 2 * Cr];
+      }
+    }
+    X[r * ip + c] = v;
+  }
+}
+
+// forward: grid (ceil(R / 32), n_win); act [nl][n_win][R][H] fp32 (the layer outputs), H3b [n_win][R][64] bf16 (the
+// last layer's output, the ones column, zeros) and, when H3lo is not null, its bf16 residual plane
 __global__ __launch_bounds__(kNT) void lv_mlp_fwd_kernel(LvArgs a, Params p, const float* __restrict__ h0,
-                                                         float* __restrict__ act, __bf16* __restrict__ H3b) {
+                                                         float* __restrict__ act, __bf16* __restrict__ H3b,
+                                                         __bf16* __restrict__ H3lo) {
   const int H = a.H, hp = H + 1, ip = a.Cin + 1;
   __shared__ float hA[kLvRows * 65], hB[kLvRows * 65], Ws[64 * 65];
   const int w = blockIdx.y, r0 = blockIdx.x * kLvRows, nr = min(kLvRows, a.R - r0);
-  const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
-  for (int idx = threadIdx.x; idx < kLvRows * a.Cin; idx += kNT) {
-    const int r = idx / a.Cin, c = idx % a.Cin;
-    hA[r * ip + c] = r < nr ? src[idx] : 0.f;
-  }
-  stage_w(Ws, hp, p.w[0], a.Cin, H);
-  __syncthreads();
+  lv_load_in(hA, ip, a, h0, w, r0, nr);
   const size_t plane = static_cast<size_t>(a.n_win) * a.R * H;
   float* ab = act + (static_cast<size_t>(w) * a.R + r0) * H;
-  dense_elu(hA, ip, a.Cin, Ws, hp, p.b[0], hB, hp, nr, H, ab, nr);
-  __syncthreads();
-  stage_w(Ws, hp, p.w[1], H, H);
-  __syncthreads();
-  dense_elu(hB, hp, H, Ws, hp, p.b[1], hA, hp, nr, H, ab + plane, nr);
-  __syncthreads();
-  stage_w(Ws, hp, p.w[2], H, H);
-  __syncthreads();
-  dense_elu(hA, hp, H, Ws, hp, p.b[2], hB, hp, nr, H, ab + 2 * plane, nr);
-  __syncthreads();
-  __bf16* ob = H3b + (static_cast<size_t>(w) * a.R + r0) * kLvC;
+  float* x = hA;
+  float* y = hB;
+  for (int l = 0; l < a.nl; ++l) {
+    const int nin = l == 0 ? a.Cin : H, xp = l == 0 ? ip : hp;
+    stage_w(Ws, hp, p.w[l], nin, H);
+    __syncthreads();
+    dense_elu(x, xp, nin, Ws, hp, p.b[l], y, hp, nr, H, ab + l * plane, nr);
+    __syncthreads();
+    float* t = x;
+    x = y;
+    y = t;
+  }
+  const size_t ofs = (static_cast<size_t>(w) * a.R + r0) * kLvC;
   for (int idx = threadIdx.x; idx < nr * kLvC; idx += kNT) {
     const int r = idx / kLvC, c = idx % kLvC;
-    ob[idx] = static_cast<__bf16>(c < H ? hB[r * hp + c] : (c == H ? 1.f : 0.f));
+    const float v = c < H ? x[r * hp + c] : (c == H ? 1.f : 0.f);
+    const __bf16 hi = static_cast<__bf16>(v);
+    H3b[ofs + idx] = hi;
+    if (H3lo) H3lo[ofs + idx] = static_cast<__bf16>(v - static_cast<float>(hi));
   }
 }
 
@@ -514,26 +537,22 @@ __global__ __launch_bounds__(kNT) void lv_mlp_bwd_kernel(LvArgs a, Params p, con
   float* Gn = Gn_;
   const int w = blockIdx.y, b = blockIdx.x, r0 = b * kLvRows, nr = min(kLvRows, a.R - r0);
   const size_t plane = static_cast<size_t>(a.n_win) * a.R * H;
-  float* out = slab + (static_cast<size_t>(w) * gridDim.x + b) * lv_n(a.Cin, H);
+  float* out = slab + (static_cast<size_t>(w) * gridDim.x + b) * lv_n(a.Cin, H, a.nl);
   const int o = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  // dz2 = dH3 * elu'(H3)
+  // dz = dH3 * elu'(H3) of the last layer
   {
-    const float* X = act + 2 * plane + (static_cast<size_t>(w) * a.R + r0) * H;
+    const float* X = act + (a.nl - 1) * plane + (static_cast<size_t>(w) * a.R + r0) * H;
     const float* D = dH3 + (static_cast<size_t>(w) * a.R + r0) * ldd;
     for (int idx = threadIdx.x; idx < kLvRows * hp; idx += kNT) {
       const int r = idx / hp, c = idx % hp;
       Gc[idx] = (r < nr && c < H) ? D[static_cast<size_t>(r) * ldd + c] * elu_d_out(X[static_cast<size_t>(r) * H + c]) : 0.f;
     }
   }
-  for (int l = 2; l >= 0; --l) {
+  for (int l = a.nl - 1; l >= 0; --l) {
     const int nin = l == 0 ? a.Cin : H, xp = l == 0 ? ip : hp;
     __syncthreads();
     if (l == 0) {
-      const float* src = h0 + static_cast<int64_t>(w) * a.in_ws + static_cast<int64_t>(r0) * a.Cin;
-      for (int idx = threadIdx.x; idx < kLvRows * a.Cin; idx += kNT) {
-        const int r = idx / a.Cin, c = idx % a.Cin;
-        Xs[r * ip + c] = r < nr ? src[idx] : 0.f;
-      }
+      lv_load_in(Xs, ip, a, h0, w, r0, nr);
     } else {
       const float* X = act + (l - 1) * plane + (static_cast<size_t>(w) * a.R + r0) * H;
       for (int idx = threadIdx.x; idx < kLvRows * hp; idx += kNT) {
@@ -576,13 +595,13 @@ __global__ __launch_bounds__(kNT) void lv_mlp_bwd_kernel(LvArgs a, Params p, con
   }
 }
 
-__global__ void lv_mlp_scatter_kernel(const float* __restrict__ red, int Cin, int H, float* gw0, float* gb0,
-                                      float* gw1, float* gb1, float* gw2, float* gb2) {
-  float* gw[3] = {gw0, gw1, gw2};
-  float* gb[3] = {gb0, gb1, gb2};
-  const int n = lv_n(Cin, H);
+__global__ void lv_mlp_scatter_kernel(const float* __restrict__ red, int Cin, int H, int nl, float* gw0, float* gb0,
+                                      float* gw1, float* gb1, float* gw2, float* gb2, float* gw3, float* gb3) {
+  float* gw[4] = {gw0, gw1, gw2, gw3};
+  float* gb[4] = {gb0, gb1, gb2, gb3};
+  const int n = lv_n(Cin, H, nl);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int l = 2;
+    int l = nl - 1;
     while (l > 0 && i < lv_off_w(l, Cin, H)) --l;
     const int ow = lv_off_w(l, Cin, H), nin = l == 0 ? Cin : H;
     if (i < ow + nin * H) gw[l][i - ow] = red[i];
@@ -594,7 +613,7 @@ __global__ void lv_mlp_scatter_kernel(const float* __restrict__ red, int Cin, in
 // Wc[r][j H + h] = conv_w[j][1 + r][h] (the conv's feature channels), zero past k H
 __global__ void lv_pack_kernel(const float* __restrict__ w3, const float* __restrict__ b3, int H, int U, int ldw,
                                __bf16* __restrict__ W3b, const float* __restrict__ cw, int R, int k, int ldc,
-                               __bf16* __restrict__ Wc) {
+                               __bf16* __restrict__ Wc, __bf16* __restrict__ Wc_lo) {
   const int64_t n1 = static_cast<int64_t>(kLvC) * ldw, n2 = static_cast<int64_t>(R) * ldc;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n1 + n2;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -606,7 +625,10 @@ __global__ void lv_pack_kernel(const float* __restrict__ w3, const float* __rest
       const int64_t e = i - n1;
       const int r = static_cast<int>(e / ldc), n = static_cast<int>(e % ldc);
       const int j = n / H, h = n % H;
-      Wc[e] = static_cast<__bf16>(j < k ? cw[(static_cast<int64_t>(j) * (1 + R) + 1 + r) * H + h] : 0.f);
+      const float v = j < k ? cw[(static_cast<int64_t>(j) * (1 + R) + 1 + r) * H + h] : 0.f;
+      const __bf16 hi = static_cast<__bf16>(v);
+      Wc[e] = hi;
+      if (Wc_lo) Wc_lo[e] = static_cast<__bf16>(v - static_cast<float>(hi));
     }
   }
 }
@@ -625,13 +647,15 @@ __global__ void lv_diag_kernel(const float* __restrict__ G, int ldg, const float
 // dG[u][j H + h] = dC[(u - j) / s][h] where (u - j) / s is a position (bf16 [U][ldg], zero elsewhere and past k H):
 // grid (ceil(ldg / 256), U), 32-bit index arithmetic
 __global__ void lv_diag_bwd_kernel(const float* __restrict__ dC, int H, int k, int s, int Lh, int ldg,
-                                   __bf16* __restrict__ dG) {
+                                   __bf16* __restrict__ dG, __bf16* __restrict__ dG_lo) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x, u = blockIdx.y;
   if (c >= ldg) return;
   const int j = c / H, h = c - j * H, t = u - j;
   float v = 0.f;
   if (j < k && t >= 0 && t % s == 0 && t / s < Lh) v = dC[(t / s) * H + h];
-  dG[static_cast<int64_t>(u) * ldg + c] = static_cast<__bf16>(v);
+  const __bf16 hi = static_cast<__bf16>(v);
+  dG[static_cast<int64_t>(u) * ldg + c] = hi;
+  if (dG_lo) dG_lo[static_cast<int64_t>(u) * ldg + c] = static_cast<__bf16>(v - static_cast<float>(hi));
 }
 
 // db[h] = sum_m dC[m][h]: one block per column, strided partial sums then the fixed-order block sum (deterministic)
@@ -736,8 +760,13 @@ int vissm_feat_bwd(const VissmFeatDesc* d, const VissmFeatParams* w, const float
 static int lv_make(const VissmLvFeatDesc* d, feat::LvArgs* a) {
   VISSM_CHECK_ARG(d && d->n_win >= 1 && d->R >= 1 && d->Cin >= 1 && d->Cin <= feat::kMaxCin && d->H >= 1 && d->H < feat::kLvC,
                   "lv_feat: bad shape (Cin <= %d, H < %d)", feat::kMaxCin, feat::kLvC);
-  VISSM_CHECK_ARG(d->in_win_stride >= static_cast<int64_t>(d->R) * d->Cin || d->n_win == 1, "lv_feat: windows of h0 overlap");
+  VISSM_CHECK_ARG(d->n_layers == 0 || d->n_layers == 3 || d->n_layers == 4, "lv_feat: n_layers %d (3 or 4)", d->n_layers);
+  VISSM_CHECK_ARG(!d->sv_diff || (d->Cin >= 2 && d->Cin % 2 == 0), "lv_feat: the difference input needs Cin = 2 Cr - 2");
+  const int64_t rows = d->sv_diff ? static_cast<int64_t>(d->R + 1) * ((d->Cin + 2) / 2) : static_cast<int64_t>(d->R) * d->Cin;
+  VISSM_CHECK_ARG(d->in_win_stride >= rows || d->n_win == 1, "lv_feat: windows of h0 overlap");
   a->n_win = d->n_win; a->R = d->R; a->Cin = d->Cin; a->H = d->H; a->in_ws = d->in_win_stride;
+  a->nl = d->n_layers == 0 ? 3 : d->n_layers;
+  a->diff = d->sv_diff ? 1 : 0;
   return VISSM_OK;
 }
 
@@ -745,19 +774,19 @@ size_t vissm_lv_mlp_workspace_size(const VissmLvFeatDesc* d) {
   feat::LvArgs a;
   if (lv_make(d, &a)) return 0;
   const int nb = (a.R + feat::kLvRows - 1) / feat::kLvRows;
-  const int n = feat::lv_n(a.Cin, a.H);
+  const int n = feat::lv_n(a.Cin, a.H, a.nl);
   return align_up(static_cast<size_t>(a.n_win) * nb * n * sizeof(float)) + align_up(n * sizeof(float));
 }
 
 int vissm_lv_mlp_fwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const float* h0, float* act, void* H3b,
-                     void* stream) {
+                     void* H3lo, void* stream) {
   feat::LvArgs a;
   int rc = lv_make(d, &a);
   if (rc) return rc;
   VISSM_CHECK_ARG(w && h0 && act && H3b, "lv_mlp_fwd: null pointer");
   dim3 grid((a.R + feat::kLvRows - 1) / feat::kLvRows, a.n_win);
   hipLaunchKernelGGL(feat::lv_mlp_fwd_kernel, grid, dim3(feat::kNT), 0, as_stream(stream), a, feat::params(w), h0, act,
-                     static_cast<__bf16*>(H3b));
+                     static_cast<__bf16*>(H3b), static_cast<__bf16*>(H3lo));
   VISSM_CHECK_LAUNCH("lv_mlp_fwd");
   return VISSM_OK;
 }
@@ -772,7 +801,7 @@ int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const f
   VISSM_CHECK_ARG(workspace && ws_bytes >= vissm_lv_mlp_workspace_size(d), "lv_mlp_bwd: workspace too small");
   hipStream_t st = as_stream(stream);
   const int nb = (a.R + feat::kLvRows - 1) / feat::kLvRows;
-  const int n = feat::lv_n(a.Cin, a.H);
+  const int n = feat::lv_n(a.Cin, a.H, a.nl);
   float* slab = static_cast<float*>(workspace);
   float* red = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                         align_up(static_cast<size_t>(a.n_win) * nb * n * sizeof(float)));
@@ -781,21 +810,22 @@ int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const f
   VISSM_CHECK_LAUNCH("lv_mlp_bwd");
   rc = launch_reduce_rows(slab, red, static_cast<int64_t>(a.n_win) * nb, n, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(feat::lv_mlp_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, a.Cin, a.H, g->w[0],
-                     g->b[0], g->w[1], g->b[1], g->w[2], g->b[2]);
+  VISSM_CHECK_ARG(a.nl < 4 || (g->w[3] && g->b[3]), "lv_mlp_bwd: four layers need the w[3] / b[3] gradients");
+  hipLaunchKernelGGL(feat::lv_mlp_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, st, red, a.Cin, a.H, a.nl,
+                     g->w[0], g->b[0], g->w[1], g->b[1], g->w[2], g->b[2], g->w[3], g->b[3]);
   VISSM_CHECK_LAUNCH("lv_mlp_scatter");
   return VISSM_OK;
 }
 
 int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
-                  int ldc, void* Wc, void* stream) {
-  VISSM_CHECK_ARG(w3 && b3 && W3b && conv_w && Wc && H >= 1 && H < feat::kLvC && U >= 1 && ldw >= U && R >= 1 &&
-                      k >= 1 && ldc >= k * H,
+                  int ldc, void* Wc, void* Wc_lo, void* stream) {
+  VISSM_CHECK_ARG((ldw == 0 || (w3 && b3 && W3b && U >= 1 && ldw >= U)) && conv_w && Wc && H >= 1 && H < feat::kLvC &&
+                      R >= 1 && k >= 1 && ldc >= k * H,
                   "lv_pack: bad argument");
   const int64_t n = static_cast<int64_t>(feat::kLvC) * ldw + static_cast<int64_t>(R) * ldc;
   hipLaunchKernelGGL(feat::lv_pack_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 16384))),
                      dim3(256), 0, as_stream(stream), w3, b3, H, U, ldw, static_cast<__bf16*>(W3b), conv_w, R, k, ldc,
-                     static_cast<__bf16*>(Wc));
+                     static_cast<__bf16*>(Wc), static_cast<__bf16*>(Wc_lo));
   VISSM_CHECK_LAUNCH("lv_pack");
   return VISSM_OK;
 }
@@ -810,14 +840,14 @@ int vissm_lv_conv_diag(const float* G, int ldg, const float* conv_b, int H, int 
   return VISSM_OK;
 }
 
-int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, float* dconv_b,
-                           void* stream) {
+int vissm_lv_conv_diag_bwd(const float* dC, int H, int k, int stride, int Lh, int U, int ldg, void* dG, void* dG_lo,
+                           float* dconv_b, void* stream) {
   VISSM_CHECK_ARG(dC && dG && dconv_b && H >= 1 && H <= 256 && k >= 1 && (stride == 1 || stride == 2) && Lh >= 1 &&
                       ldg >= k * H && stride * (Lh - 1) + k <= U,
                   "lv_conv_diag_bwd: bad argument");
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(feat::lv_diag_bwd_kernel, dim3((ldg + 255) / 256, U), dim3(256), 0, st, dC, H, k, stride, Lh, ldg,
-                     static_cast<__bf16*>(dG));
+                     static_cast<__bf16*>(dG), static_cast<__bf16*>(dG_lo));
   VISSM_CHECK_LAUNCH("lv_conv_diag_bwd");
   // the conv bias gradient: column sums of dC over its Lh rows (a single sequential pass per column was 0.65 ms of
   // dependent loads at Lh = 5000)

@@ -15,6 +15,11 @@
 // 20 banks); a K-major one as [k][row] with 288-byte rows, read with ds_read_b64_tr_b16 (the same k order; row stride
 // 8 banks mod 64).  Epilogues: fp32 store, ELU -> bf16, x elu'(y) of a bf16 ELU output -> bf16.  Split-K
 // (gridDim.z > 1) writes per-split fp32 partials that a fixed-order pass sums (deterministic).
+//
+// Split-bf16 form (vissm_gemm_bf16x3; SV's window-shared conv, SV_dense.py:56-62, at fp32-class accuracy): the K loop
+// runs over three passes of the K range, (A_hi, B_hi), (A_hi, B_lo), (A_lo, B_hi), into the same accumulators; each
+// pass is padded to a whole number of K steps, so a step never straddles two passes and split-K divides the 3 K
+// range like any other.
 #include "common.hpp"
 
 namespace vissm {
@@ -42,7 +47,8 @@ constexpr int IMG = 128 * RP > BK * CP ? 128 * RP : BK * CP;   // elements per o
 
 struct KArgs {
   int64_t M, N, K, lda, ldb, ldc;
-  int64_t kper;      // K range per split (multiple of BK)
+  int64_t Kp;        // one pass's K range padded to a multiple of BK (the loop runs over npass Kp)
+  int64_t kper;      // range per split of the npass Kp loop (multiple of BK)
   int64_t slab;      // elements between split partials (split-K)
 };
 
@@ -113,9 +119,12 @@ __device__ __forceinline__ float elu_acc(float x) { return x > 0.f ? x : expm1f(
 
 // EPI: 0 fp32 store (split-K: partial z at C + z slab), 1 ELU -> bf16, 2 x elu'(aux) -> bf16 (aux: bf16 ELU output,
 // same layout as C)
-template <bool AKM, bool BKM, int EPI>
+// X3: the split-bf16 form (A2 / B2 the lo planes; passes above)
+template <bool AKM, bool BKM, int EPI, bool X3 = false>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __restrict__ A, const __bf16* __restrict__ B,
-                                                     void* __restrict__ Cv, const __bf16* __restrict__ aux) {
+                                                     void* __restrict__ Cv, const __bf16* __restrict__ aux,
+                                                     const __bf16* __restrict__ A2 = nullptr,
+                                                     const __bf16* __restrict__ B2 = nullptr) {
   // the two operands' double buffers in one array (the bf16 epilogue stages its 4 x 8.5 KB through all of it)
   __shared__ __attribute__((aligned(16))) __bf16 smem[4][IMG];
   __bf16(*sa)[IMG] = smem;
@@ -136,7 +145,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
   }
   const int64_t m0 = static_cast<int64_t>(mt) * BM, n0 = static_cast<int64_t>(nt) * BN;
   const int64_t kb = static_cast<int64_t>(blockIdx.z) * a.kper;
-  const int64_t ke = min(a.K, kb + a.kper);
+  const int64_t ke = min(X3 ? 3 * a.Kp : a.K, kb + a.kper);
+  // K step at loop position kk: its pass's operands and its k within the pass (X3; block-uniform)
+  auto load = [&](Stage<AKM>& la, Stage<BKM>& lb, int64_t kk) {
+    if constexpr (X3) {
+      const int pass = static_cast<int>(kk / a.Kp);
+      const int64_t k0 = kk - pass * a.Kp;
+      la.load(pass == 2 ? A2 : A, a.lda, m0, k0, a.M, a.K);
+      lb.load(pass == 1 ? B2 : B, a.ldb, n0, k0, a.N, a.K);
+    } else {
+      la.load(A, a.lda, m0, kk, a.M, ke);
+      lb.load(B, a.ldb, n0, kk, a.N, ke);
+    }
+  };
   f4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -146,8 +167,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
   Stage<BKM> lb;
   const int nk = static_cast<int>((ke - kb + BK - 1) / BK);
   if (nk > 0) {
-    la.load(A, a.lda, m0, kb, a.M, ke);
-    lb.load(B, a.ldb, n0, kb, a.N, ke);
+    load(la, lb, kb);
     la.store(sa[0]);
     lb.store(sb[0]);
   }
@@ -155,10 +175,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
-    if (more) {
-      la.load(A, a.lda, m0, kb + static_cast<int64_t>(kt + 1) * BK, a.M, ke);
-      lb.load(B, a.ldb, n0, kb + static_cast<int64_t>(kt + 1) * BK, a.N, ke);
-    }
+    if (more) load(la, lb, kb + static_cast<int64_t>(kt + 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       bf8 af[4], bfr[4];
@@ -264,49 +281,50 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
 using namespace vissm;
 using namespace vissm::gemm;
 
-extern "C" {
-
-size_t vissm_gemm_workspace_size(const VissmGemmDesc* d) {
-  if (!d || d->split_k <= 1) return 0;
-  return align_up(static_cast<size_t>(d->split_k) * d->M * d->N * sizeof(float));
-}
-
-int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* C, const void* aux, void* workspace,
-                    size_t ws_bytes, void* stream) {
-  VISSM_CHECK_ARG(d && A && B && C, "gemm_bf16: null argument");
-  VISSM_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "gemm_bf16: negative size");
+// shared argument checks and launch of both entry points (x3: the split-bf16 form, fp32 epilogue)
+static int gemm_launch(const VissmGemmDesc* d, const void* A, const void* A2, const void* B, const void* B2, void* C,
+                       const void* aux, void* workspace, size_t ws_bytes, void* stream, bool x3) {
+  const char* nm = x3 ? "gemm_bf16x3" : "gemm_bf16";
+  VISSM_CHECK_ARG(d && A && B && C && (!x3 || (A2 && B2)), "%s: null argument", nm);
+  VISSM_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "%s: negative size", nm);
   if (d->M == 0 || d->N == 0) return VISSM_OK;
-  VISSM_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "gemm_bf16: leading dimensions must be multiples of 8");
-  VISSM_CHECK_ARG((reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0,
-                  "gemm_bf16: A and B must be 16-byte aligned");
+  VISSM_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "%s: leading dimensions must be multiples of 8", nm);
+  VISSM_CHECK_ARG(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(A2) |
+                    reinterpret_cast<uintptr_t>(B2)) & 15) == 0,
+                  "%s: operands must be 16-byte aligned", nm);
   VISSM_CHECK_ARG(d->lda >= (d->a_kmajor ? d->M : d->K) && d->ldb >= (d->b_kmajor ? d->N : d->K),
-                  "gemm_bf16: leading dimension below the row length");
-  VISSM_CHECK_ARG(d->ldc >= d->N, "gemm_bf16: ldc < N");
-  VISSM_CHECK_ARG(d->epilogue >= VISSM_GEMM_F32 && d->epilogue <= VISSM_GEMM_DELU_BF16, "gemm_bf16: epilogue");
-  VISSM_CHECK_ARG(d->epilogue != VISSM_GEMM_DELU_BF16 || aux, "gemm_bf16: the elu' epilogue needs aux");
+                  "%s: leading dimension below the row length", nm);
+  VISSM_CHECK_ARG(d->ldc >= d->N, "%s: ldc < N", nm);
+  VISSM_CHECK_ARG(d->epilogue >= VISSM_GEMM_F32 && d->epilogue <= VISSM_GEMM_DELU_BF16, "%s: epilogue", nm);
+  VISSM_CHECK_ARG(!x3 || d->epilogue == VISSM_GEMM_F32, "%s: the split-bf16 form has the fp32 epilogue only", nm);
+  VISSM_CHECK_ARG(d->epilogue != VISSM_GEMM_DELU_BF16 || aux, "%s: the elu' epilogue needs aux", nm);
   const int split = d->split_k > 1 ? d->split_k : 1;
   VISSM_CHECK_ARG(split == 1 || (d->epilogue == VISSM_GEMM_F32 && d->ldc == d->N),
-                  "gemm_bf16: split-K needs the fp32 epilogue and ldc == N");
-  VISSM_CHECK_ARG(split == 1 || (workspace && ws_bytes >= vissm_gemm_workspace_size(d)),
-                  "gemm_bf16: workspace too small");
+                  "%s: split-K needs the fp32 epilogue and ldc == N", nm);
+  VISSM_CHECK_ARG(split == 1 || (workspace && ws_bytes >= vissm_gemm_workspace_size(d)), "%s: workspace too small", nm);
   hipStream_t st = as_stream(stream);
   KArgs a;
   a.M = d->M; a.N = d->N; a.K = d->K; a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
-  a.kper = ((d->K + split - 1) / split + BK - 1) / BK * BK;
+  a.Kp = (d->K + BK - 1) / BK * BK;
+  const int64_t krange = x3 ? 3 * a.Kp : d->K;
+  a.kper = ((krange + split - 1) / split + BK - 1) / BK * BK;
   if (a.kper <= 0) a.kper = BK;
   a.slab = d->M * d->N;
-  const int nz = static_cast<int>((d->K + a.kper - 1) / a.kper) > 0 ? static_cast<int>((d->K + a.kper - 1) / a.kper) : 1;
+  const int nz = static_cast<int>((krange + a.kper - 1) / a.kper) > 0 ? static_cast<int>((krange + a.kper - 1) / a.kper) : 1;
   dim3 grid(static_cast<unsigned>((d->N + BN - 1) / BN), static_cast<unsigned>((d->M + BM - 1) / BM),
             static_cast<unsigned>(split == 1 ? 1 : nz));
   void* out = split == 1 ? C : workspace;
   const __bf16* pa = static_cast<const __bf16*>(A);
   const __bf16* pb = static_cast<const __bf16*>(B);
+  const __bf16* pa2 = static_cast<const __bf16*>(A2);
+  const __bf16* pb2 = static_cast<const __bf16*>(B2);
   const __bf16* px = static_cast<const __bf16*>(aux);
 #define GEMM_EPI(AK, BKk)                                                                                      \
   do {                                                                                                       \
-    if (d->epilogue == VISSM_GEMM_F32) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0>), grid, dim3(NT), 0, st, a, pa, pb, out, px); \
-    else if (d->epilogue == VISSM_GEMM_ELU_BF16) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 1>), grid, dim3(NT), 0, st, a, pa, pb, out, px); \
-    else hipLaunchKernelGGL((gemm_kernel<AK, BKk, 2>), grid, dim3(NT), 0, st, a, pa, pb, out, px);            \
+    if (x3) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0, true>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    else if (d->epilogue == VISSM_GEMM_F32) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    else if (d->epilogue == VISSM_GEMM_ELU_BF16) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 1>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    else hipLaunchKernelGGL((gemm_kernel<AK, BKk, 2>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2);   \
   } while (0)
   if (d->a_kmajor) {
     if (d->b_kmajor) GEMM_EPI(true, true);
@@ -316,9 +334,28 @@ int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* 
     else GEMM_EPI(false, false);
   }
 #undef GEMM_EPI
-  VISSM_CHECK_LAUNCH("gemm_bf16");
+  VISSM_CHECK_LAUNCH(nm);
   if (split > 1) return launch_reduce_rows(static_cast<const float*>(workspace), static_cast<float*>(C), grid.z, d->M * d->N, st);
   return VISSM_OK;
+}
+
+extern "C" {
+
+size_t vissm_gemm_workspace_size(const VissmGemmDesc* d) {
+  if (!d || d->split_k <= 1) return 0;
+  return align_up(static_cast<size_t>(d->split_k) * d->M * d->N * sizeof(float));
+}
+
+int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* C, const void* aux, void* workspace,
+                    size_t ws_bytes, void* stream) {
+  return gemm_launch(d, A, nullptr, B, nullptr, C, aux, workspace, ws_bytes, stream, false);
+}
+
+size_t vissm_gemm_bf16x3_workspace_size(const VissmGemmDesc* d) { return vissm_gemm_workspace_size(d); }
+
+int vissm_gemm_bf16x3(const VissmGemmDesc* d, const void* A_hi, const void* A_lo, const void* B_hi, const void* B_lo,
+                      void* C, void* workspace, size_t ws_bytes, void* stream) {
+  return gemm_launch(d, A_hi, A_lo, B_hi, B_lo, C, nullptr, workspace, ws_bytes, stream, true);
 }
 
 }  // extern "C"

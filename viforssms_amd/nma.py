@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, lv_feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
+from .ops import (FlowShape, kernel_precision, ma_flow, feat_conv, lv_feat_conv, sv_feat_conv, normal_base, normal_base_dev, base_logprob, elbo_terms,
                   ElboFeeds, AdamaxKernel, ar_fused_supported, ar_last_flow_fused, elbo_values_and_theta_grad,
                   elbo_values_grad, theta_branch_bwd, theta_branch_fwd)
 from .params import ParamStore, glorot_uniform
@@ -285,6 +285,14 @@ class IAF:
             return lv_feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"),
                                 p("feat1/bias"), p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"),
                                 p("feat3/bias"), p("conv/kernel"), p("conv/bias"))
+        # SV (k = 50) at the non-fp32 precisions: the hand-written branch (ops.sv_feat_conv: vissm_lv_mlp_* with the
+        # first-difference input, the conv as one split-bf16 matrix-core GEMM each way); VISSM_SV_FEAT=torch selects
+        # the torch form (fp32 layers, linear_x3 conv)
+        if f == "sv" and ts.is_cuda and gemm == "x3" and os.environ.get("VISSM_SV_FEAT", "hip") != "torch":
+            p = self._p
+            return sv_feat_conv(ts, s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
+                                p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
+                                p("conv/kernel"), p("conv/bias"))
         return self.conv_shared(self.features(ts), Lh, s, gemm=gemm)
 
     def theta_factors(self, theta: torch.Tensor):
@@ -641,9 +649,14 @@ class Engine:
         fp32-class) at the parity precisions bf16x3 / bf16x3f / bf16x2f, fp32 otherwise (None).  For LV at a
         non-fp32 precision only, Engine.feature_gemm_override or VISSM_FEATURE_GEMM = bf16 | x3 | fp32 replaces the
         choice (A/B timing; tests that isolate the flow kernels from the bf16 rounding of these GEMMs); fp32 runs
-        and the other families never change arithmetic."""
-        if self.precision == _lib.VISSM_PREC_FP32 or self.mdef.family != "lv":
+        and the other families never change arithmetic.  SV (k = 50, a [L x 50] by [50 x 2500] conv product) runs its
+        conv in the split-bf16 form at every non-fp32 precision ("x3": the hand-written branch, window_conv;
+        VISSM_FEATURE_GEMM=fp32 restores the torch fp32 form for it too)."""
+        if self.precision == _lib.VISSM_PREC_FP32 or self.mdef.family not in ("lv", "sv"):
             return None
+        if self.mdef.family == "sv":
+            mode = getattr(self, "feature_gemm_override", None) or os.environ.get("VISSM_FEATURE_GEMM")
+            return None if mode == "fp32" else "x3"
         mode = getattr(self, "feature_gemm_override", None) or os.environ.get("VISSM_FEATURE_GEMM")
         if mode:
             if mode not in ("bf16", "x3", "fp32"):

@@ -293,6 +293,18 @@ def gemm_bf16(M: int, N: int, K: int, A, lda: int, a_kmajor: bool, B, ldb: int, 
                               ptr(ws) if ws is not None else None, nb, _lib.stream_handle(C.device)), "vissm_gemm_bf16")
 
 
+def gemm_bf16x3(M: int, N: int, K: int, A, A_lo, lda: int, a_kmajor: bool, B, B_lo, ldb: int, b_kmajor: bool, C,
+                ldc: int, split_k: int = 1):
+    """C = A_hi B_hi + A_hi B_lo + A_lo B_hi (fp32 C): the split-bf16 form of gemm_bf16, fp32-class products"""
+    lib = _lib.load()
+    d = _lib.GemmDesc(M, N, K, lda, ldb, ldc, int(a_kmajor), int(b_kmajor), _lib.GEMM_F32, split_k)
+    nb = lib.vissm_gemm_bf16x3_workspace_size(ctypes.byref(d))
+    ws = _workspace(nb, C.device) if nb else None
+    check(lib.vissm_gemm_bf16x3(ctypes.byref(d), ptr(A), ptr(A_lo), ptr(B), ptr(B_lo), ptr(C),
+                                ptr(ws) if ws is not None else None, nb, _lib.stream_handle(C.device)),
+          "vissm_gemm_bf16x3")
+
+
 def _r8(n: int) -> int:
     return (n + 7) // 8 * 8
 
@@ -322,14 +334,15 @@ class LvFeatConvFn(torch.autograd.Function):
         dev = h0.device
         Up, NC = _r8(U), _r8(k * H)
         lib, st = _lib.load(), _lib.stream_handle(dev)
-        d = _lib.LvFeatDesc(n_win, R, Cin, H, h0.stride(0) if n_win > 1 else R * Cin)
+        d = _lib.LvFeatDesc(n_win, R, Cin, H, h0.stride(0) if n_win > 1 else R * Cin, 3, 0)
         p = _feat_params(ws)
         act = torch.empty(3, n_win, R, H, dtype=torch.float32, device=dev)
         H3b = torch.empty(n_win, R, 64, dtype=torch.bfloat16, device=dev)
-        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(act), ptr(H3b), st), "vissm_lv_mlp_fwd")
+        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(act), ptr(H3b), None, st),
+              "vissm_lv_mlp_fwd")
         W3b = torch.empty(64, Up, dtype=torch.bfloat16, device=dev)
         Wc = torch.empty(R, NC, dtype=torch.bfloat16, device=dev)
-        check(lib.vissm_lv_pack(ptr(W3), ptr(b3), H, U, Up, ptr(W3b), ptr(conv_w), R, k, NC, ptr(Wc), st),
+        check(lib.vissm_lv_pack(ptr(W3), ptr(b3), H, U, Up, ptr(W3b), ptr(conv_w), R, k, NC, ptr(Wc), None, st),
               "vissm_lv_pack")
         D = torch.empty(n_win, R, Up, dtype=torch.bfloat16, device=dev)
         G = torch.empty(U, NC, dtype=torch.float32, device=dev)
@@ -356,7 +369,7 @@ class LvFeatConvFn(torch.autograd.Function):
         dH3 = torch.empty(n_win, R, 64, dtype=torch.float32, device=dev)
         dcb = torch.empty(n_win, H, dtype=torch.float32, device=dev)
         for w in range(n_win):
-            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG), ptr(dcb[w]), st),
+            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG), None, ptr(dcb[w]), st),
                   "vissm_lv_conv_diag_bwd")
             gemm_bf16(R, U, NC, Wc, NC, False, dG, NC, False, dP, Up, _lib.GEMM_DELU_BF16, aux=D[w])
             gemm_bf16(R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, _lib.GEMM_F32)
@@ -380,6 +393,90 @@ class LvFeatConvFn(torch.autograd.Function):
 
 def lv_feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
     return LvFeatConvFn.apply(h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+
+
+class SvFeatConvFn(torch.autograd.Function):
+    """Stochastic volatility's window-shared conv input C [n_win, Lh, H] (SV_dense.py:50-62): the four dense + ELU
+    layers over the window's time features with their first differences (the input assembly inside the kernel:
+    vissm_lv_mlp_* at n_layers = 4, sv_diff = 1; fp32), then the conv over the 50 feature channels at kernel_len 50
+    as one split-bf16 matrix-core GEMM G = F [Wc_0 | .. | Wc_{k-1}] (vissm_gemm_bf16x3: fp32-class products, the
+    torch form's fp32 arithmetic to ~1e-6) and its diagonal sum; backward: dG (hi / lo planes), dF = dG Wc^T and
+    dWc = F^T dG the same way, then the four layers' gradients.  ts [n_win, L, Cr] gets no gradient (data)."""
+
+    @staticmethod
+    def forward(ctx, ts, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+        ws = (W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+        _require_gpu(*ws)
+        n_win, L, Cr = ts.shape
+        if ts.dtype != torch.float32 or ts.stride(2) != 1 or ts.stride(1) != Cr:
+            ts = ts.contiguous()
+        _require_gpu(ts)
+        R, Cin = L - 1, 2 * Cr - 2
+        H, k = W0.shape[1], conv_w.shape[0]
+        if (tuple(W0.shape) != (Cin, H) or tuple(W3.shape) != (H, H) or tuple(conv_w.shape) != (k, 1 + H, H)
+                or s * (Lh - 1) + k > R or H >= 64):
+            raise _lib.VissmError(f"sv_feat: ts {tuple(ts.shape)}, W0 {tuple(W0.shape)}, conv_w {tuple(conv_w.shape)}, "
+                                  f"Lh {Lh}, s {s}: shapes do not match")
+        dev = ts.device
+        NC = k * H
+        NCp = _r8(NC)
+        lib, st = _lib.load(), _lib.stream_handle(dev)
+        d = _lib.LvFeatDesc(n_win, R, Cin, H, ts.stride(0) if n_win > 1 else L * Cr, 4, 1)
+        act = torch.empty(4, n_win, R, H, dtype=torch.float32, device=dev)
+        Fh = torch.empty(n_win, R, 64, dtype=torch.bfloat16, device=dev)
+        Fl = torch.empty_like(Fh)
+        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(_feat_params(ws)), ptr(ts), ptr(act), ptr(Fh),
+                                   ptr(Fl), st), "vissm_lv_mlp_fwd")
+        Wch = torch.empty(H, NCp, dtype=torch.bfloat16, device=dev)
+        Wcl = torch.empty_like(Wch)
+        check(lib.vissm_lv_pack(None, None, H, 0, 0, None, ptr(conv_w), H, k, NCp, ptr(Wch), ptr(Wcl), st),
+              "vissm_lv_pack")
+        G = torch.empty(R, NCp, dtype=torch.float32, device=dev)
+        C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=dev)
+        for w in range(n_win):
+            gemm_bf16x3(R, NC, H, Fh[w], Fl[w], 64, False, Wch, Wcl, NCp, True, G, NCp)
+            check(lib.vissm_lv_conv_diag(ptr(G), NCp, ptr(conv_b), H, k, s, Lh, ptr(C[w]), st), "vissm_lv_conv_diag")
+        ctx.save_for_backward(ts, act, Fh, Fl, Wch, Wcl, *ws)
+        ctx.dims = (d, n_win, R, H, k, s, Lh, NC, NCp)
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        ts, act, Fh, Fl, Wch, Wcl, *ws = ctx.saved_tensors
+        d, n_win, R, H, k, s, Lh, NC, NCp = ctx.dims
+        dev = dC.device
+        dC = dC.contiguous()
+        lib, st = _lib.load(), _lib.stream_handle(dev)
+        dGh = torch.empty(R, NCp, dtype=torch.bfloat16, device=dev)
+        dGl = torch.empty_like(dGh)
+        dF = torch.empty(n_win, R, H, dtype=torch.float32, device=dev)
+        dWc = torch.empty(n_win, H, NC, dtype=torch.float32, device=dev)
+        dcb = torch.empty(n_win, H, dtype=torch.float32, device=dev)
+        for w in range(n_win):
+            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, R, NCp, ptr(dGh), ptr(dGl), ptr(dcb[w]), st),
+                  "vissm_lv_conv_diag_bwd")
+            # dF = dG Wc^T (K = k H, split over it: R / 128 row tiles alone would leave the chip empty)
+            gemm_bf16x3(R, H, NC, dGh, dGl, NCp, False, Wch, Wcl, NCp, False, dF[w], H, split_k=16)
+            # dWc = F^T dG (K = R)
+            gemm_bf16x3(H, NC, R, Fh[w], Fl[w], 64, True, dGh, dGl, NCp, True, dWc[w], NC, split_k=8)
+        if n_win > 1:
+            dWc, dcb = dWc.sum(0, keepdim=True), dcb.sum(0, keepdim=True)
+        gr = [torch.empty_like(t) for t in ws[:8]]
+        dconv_w = torch.empty_like(ws[8])
+        check(lib.vissm_lv_conv_wscatter(ptr(dWc[0]), NC, H, k, H, ptr(dconv_w), st), "vissm_lv_conv_wscatter")
+        g = _lib.FeatGrads((ctypes.c_void_p * 4)(ptr(gr[0]), ptr(gr[2]), ptr(gr[4]), ptr(gr[6])),
+                           (ctypes.c_void_p * 4)(ptr(gr[1]), ptr(gr[3]), ptr(gr[5]), ptr(gr[7])), None, None)
+        nb = lib.vissm_lv_mlp_workspace_size(ctypes.byref(d))
+        if nb == 0:
+            raise _lib.VissmError(f"vissm_lv_mlp_workspace_size failed: {lib.vissm_last_error().decode()}")
+        wsb = _workspace(nb, dev)
+        check(lib.vissm_lv_mlp_bwd(ctypes.byref(d), ctypes.byref(_feat_params(ws)), ptr(ts), ptr(act), ptr(dF), H,
+                                   ctypes.byref(g), ptr(wsb), nb, st), "vissm_lv_mlp_bwd")
+        return (None, None, None, *gr, dconv_w, dcb[0])
+
+
+def sv_feat_conv(ts, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+    return SvFeatConvFn.apply(ts, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
 
 
 class MAFlowFn(torch.autograd.Function):
