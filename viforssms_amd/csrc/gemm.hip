@@ -37,6 +37,16 @@ typedef __attribute__((address_space(3))) bf4 lds_bf4;
 #ifndef VISSM_GEMM_BK
 #define VISSM_GEMM_BK 32
 #endif
+// register prefetch depth: 1 = the global loads of step k + 1 are issued while step k computes; 2 = step k + 2 (two
+// register sets, +16 VGPRs) measured slower: LV-cfg GEMM time 15.3 -> 16.8 ms per 54 launches, 15.7 at <= 168 VGPRs
+// (three blocks per CU) -- the loads' latency is not what holds these tiles (profiles/r06/gemm_pf/)
+#ifndef VISSM_GEMM_PF
+#define VISSM_GEMM_PF 1
+#endif
+// blocks per CU the register allocation is held to (3: <= 168 VGPRs)
+#ifndef VISSM_GEMM_MINB
+#define VISSM_GEMM_MINB 2
+#endif
 constexpr int BM = 128, BN = 128, BK = VISSM_GEMM_BK, NT = 256;
 constexpr int KS = BK / 32;    // MFMA k-steps per K-step
 constexpr int CPR = BK / 8;    // 16-byte chunks per [row][k] image row
@@ -121,7 +131,7 @@ __device__ __forceinline__ float elu_acc(float x) { return x > 0.f ? x : expm1f(
 // same layout as C)
 // X3: the split-bf16 form (A2 / B2 the lo planes; passes above)
 template <bool AKM, bool BKM, int EPI, bool X3 = false>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+__global__ __launch_bounds__(NT, VISSM_GEMM_MINB) void gemm_kernel(KArgs a, const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                      void* __restrict__ Cv, const __bf16* __restrict__ aux,
                                                      const __bf16* __restrict__ A2 = nullptr,
                                                      const __bf16* __restrict__ B2 = nullptr) {
@@ -163,19 +173,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  Stage<AKM> la;
-  Stage<BKM> lb;
   const int nk = static_cast<int>((ke - kb + BK - 1) / BK);
-  if (nk > 0) {
-    load(la, lb, kb);
-    la.store(sa[0]);
-    lb.store(sb[0]);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load(la, lb, kb + static_cast<int64_t>(kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       bf8 af[4], bfr[4];
@@ -188,12 +187,51 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(KArgs a, const __bf16* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
     }
+  };
+  Stage<AKM> la;
+  Stage<BKM> lb;
+  if (nk > 0) {
+    load(la, lb, kb);
+    la.store(sa[0]);
+    lb.store(sb[0]);
+  }
+#if VISSM_GEMM_PF >= 2
+  Stage<AKM> la1;
+  Stage<BKM> lb1;
+  if (nk > 1) load(la1, lb1, kb + BK);
+  __syncthreads();
+  // step kt: (ra, rb) held step kt (in LDS by now) and take the loads of step kt + 2; (qa, qb) hold step kt + 1,
+  // stored into the other LDS buffer after the compute; the two register sets swap roles every step
+  auto step = [&](int kt, Stage<AKM>& ra, Stage<BKM>& rb, Stage<AKM>& qa, Stage<BKM>& qb) {
+    const int cur = kt & 1;
+    if (kt + 2 < nk) load(ra, rb, kb + static_cast<int64_t>(kt + 2) * BK);
+    compute(cur);
+    if (kt + 1 < nk) {
+      qa.store(sa[cur ^ 1]);
+      qb.store(sb[cur ^ 1]);
+    }
+    __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, la, lb, la1, lb1);
+    step(kt + 1, la1, lb1, la, lb);
+  }
+  if (kt < nk) step(kt, la, lb, la1, lb1);
+#else
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load(la, lb, kb + static_cast<int64_t>(kt + 1) * BK);
+    compute(cur);
     if (more) {
       la.store(sa[cur ^ 1]);
       lb.store(sb[cur ^ 1]);
     }
     __syncthreads();
   }
+#endif
   // epilogue: lane (g, c) of block (i, j) holds C[m = base_m + 16 i + 4 g + r][n = base_n + 16 j + c]
   if constexpr (EPI != 0) {
     // bf16 outputs through LDS (the operand buffers are free after the loop's last barrier): each wave writes its

@@ -347,9 +347,10 @@ class LvFeatConvFn(torch.autograd.Function):
         D = torch.empty(n_win, R, Up, dtype=torch.bfloat16, device=dev)
         G = torch.empty(U, NC, dtype=torch.float32, device=dev)
         C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=dev)
+        sk = int(os.environ.get("VISSM_LV_SPLIT", "5"))
         for w in range(n_win):
             gemm_bf16(R, U, 64, H3b[w], 64, False, W3b, Up, True, D[w], Up, _lib.GEMM_ELU_BF16)
-            gemm_bf16(U, NC, R, D[w], Up, True, Wc, NC, True, G, NC, _lib.GEMM_F32)
+            gemm_bf16(U, NC, R, D[w], Up, True, Wc, NC, True, G, NC, _lib.GEMM_F32, split_k=sk)
             check(lib.vissm_lv_conv_diag(ptr(G), NC, ptr(conv_b), H, k, s, Lh, ptr(C[w]), st), "vissm_lv_conv_diag")
         ctx.save_for_backward(h0, act, H3b, D, W3b, Wc, *ws)
         ctx.dims = (d, n_win, R, H, U, k, s, Lh, Up, NC)
@@ -372,9 +373,11 @@ class LvFeatConvFn(torch.autograd.Function):
             check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG), None, ptr(dcb[w]), st),
                   "vissm_lv_conv_diag_bwd")
             gemm_bf16(R, U, NC, Wc, NC, False, dG, NC, False, dP, Up, _lib.GEMM_DELU_BF16, aux=D[w])
-            gemm_bf16(R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, _lib.GEMM_F32)
-            gemm_bf16(64, U, R, H3b[w], 64, True, dP, Up, True, dW3b[w], U, _lib.GEMM_F32, split_k=4)
-            gemm_bf16(R, 64, U, dP, Up, False, W3b, Up, False, dH3[w], 64, _lib.GEMM_F32, split_k=4)
+            gemm_bf16(R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, _lib.GEMM_F32,
+                      split_k=int(os.environ.get("VISSM_LV_SPLIT", "5")))
+            sw = int(os.environ.get("VISSM_LV_SPLIT_W3", "8"))
+            gemm_bf16(64, U, R, H3b[w], 64, True, dP, Up, True, dW3b[w], U, _lib.GEMM_F32, split_k=sw)
+            gemm_bf16(R, 64, U, dP, Up, False, W3b, Up, False, dH3[w], 64, _lib.GEMM_F32, split_k=sw)
         if n_win > 1:   # (the reference's LV windows: one per step at the benchmark shapes)
             dWc, dW3b, dcb = dWc.sum(0, keepdim=True), dW3b.sum(0, keepdim=True), dcb.sum(0, keepdim=True)
         gr = [torch.empty_like(t) for t in ws[:6]]
