@@ -92,14 +92,29 @@ class ParamStore:
             if g is None or g.data_ptr() != self.grad[a:a + sz].data_ptr():
                 t.grad = self.grad[a:a + sz].view(t.shape)
 
+    def release_grads(self):
+        """Drop every variable's .grad view before a backward whose gradients nobody reads until sync_grads: autograd
+        then keeps each variable's incoming gradient tensor as its .grad (no kernel) instead of adding it into the
+        zeroed flat view (one element-wise launch per variable: ~160 per SV step, ~0.7 ms); sync_grads moves them
+        into the flat buffer in a few multi-tensor copies.  The flat buffer is already zero (zero_grad), so a
+        variable that receives no gradient keeps its zero slice."""
+        for t in self.tensors.values():
+            t.grad = None
+
     def sync_grads(self):
-        """Copy any .grad that autograd re-allocated back into the flat buffer (normally a no-op)."""
+        """Copy any .grad that autograd re-allocated (or that release_grads let it allocate) back into the flat
+        buffer, batched into multi-tensor copies, and point the .grad at the flat views again."""
+        dst, src = [], []
         for name, t in self.tensors.items():
             a, sz = self.offsets[name]
             g = t.grad
             if g is not None and g.data_ptr() != self.grad[a:a + sz].data_ptr():
-                self.grad[a:a + sz].copy_(g.reshape(-1))
-                t.grad = self.grad[a:a + sz].view(t.shape)
+                v = self.grad[a:a + sz].view(t.shape)
+                dst.append(v)
+                src.append(g)
+                t.grad = v
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def state_numpy(self) -> Dict[str, np.ndarray]:
         return {n: self.tensors[n].detach().cpu().numpy() for n in self._specs}

@@ -284,9 +284,13 @@ class VISSMBase:
         post-accumulate hook of its last variable, so it runs over xGMI while the earlier flows' backward
         kernels still execute; _reduce_grads waits for them.  shared: the step sums the
         window-shared gradients through dC, so their variables are in no bucket."""
-        if (self.dist.world <= 1 or not self.overlap_allreduce
-                or (self.store.grad.is_cuda and torch.cuda.is_current_stream_capturing())):
+        capturing = self.store.grad.is_cuda and torch.cuda.is_current_stream_capturing()
+        if self.dist.world <= 1 or not self.overlap_allreduce or capturing:
             self._ov = None   # (a captured step keeps the single blocking all-reduce)
+            if not capturing and os.environ.get("VISSM_GRAD_RELEASE", "1") != "0":
+                # no hook reads a .grad before _reduce_grads' sync_grads: let autograd keep the gradient tensors
+                # instead of adding each into its zeroed flat view (params.ParamStore.release_grads)
+                self.store.release_grads()
             return
         st = self.store
         if not getattr(self, "_ov_hooked", False):
