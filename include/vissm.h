@@ -389,10 +389,10 @@ int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const f
                      const float* dH3, int ld_dH3, const VissmFeatGrads* g, void* workspace, size_t ws_bytes,
                      void* stream);
 /* W3b [64][ldw] bf16 (rows < H: w3 [H][U], row H: b3, zeros; columns >= U zero; ldw = 0: none, w3 / b3 / W3b
- * unused) and Wc [R][ldc] bf16 (Wc[r][j H + h] = conv_w[j][1 + r][h], zero for columns >= k H; Wc_lo, when not null,
- * its bf16 residual plane) */
-int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
-                  int ldc, void* Wc, void* Wc_lo, void* stream);
+ * unused) and Wc [R][ldc] bf16 (Wc[r][j H + h] = conv_w[j][1 + r][h], zero for columns >= k H); W3b_lo / Wc_lo,
+ * when not null, their bf16 residual planes (the split-bf16 GEMM's operands) */
+int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, void* W3b_lo, const float* conv_w,
+                  int R, int k, int ldc, void* Wc, void* Wc_lo, void* stream);
 /* C[m][h] = conv_b[h] + sum_{j<k} G[s m + j][j H + h], G [U][ldg] fp32, m < Lh */
 int vissm_lv_conv_diag(const float* G, int ldg, const float* conv_b, int H, int k, int stride, int Lh, float* C,
                        void* stream);
@@ -424,10 +424,11 @@ int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* 
                     size_t ws_bytes, void* stream);
 /* The split-bf16 form (fp32-class products: the operands' hi / lo bf16 planes, x = hi + lo to ~2^-16, the same
  * layouts): C = A_hi B_hi + A_hi B_lo + A_lo B_hi, one launch whose K loop runs the three passes (split-K divides
- * the 3 K range).  The fp32 epilogue only. */
+ * the 3 K range).  Every epilogue: the bf16 ones write C as a hi / lo plane pair (the lo plane at C + M ldc) and
+ * read aux the same way (y = aux_hi + aux_lo). */
 size_t vissm_gemm_bf16x3_workspace_size(const VissmGemmDesc* d);
 int vissm_gemm_bf16x3(const VissmGemmDesc* d, const void* A_hi, const void* A_lo, const void* B_hi, const void* B_lo,
-                      void* C, void* workspace, size_t ws_bytes, void* stream);
+                      void* C, const void* aux, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Window gather: the per-step feed assembly of VI_SSM.train (AR.py:267-288;

@@ -96,6 +96,36 @@ def _torch_form(h0, ws, s, Lh, lin):
 
 
 @pytest.mark.parametrize("R,U,k,s", [(301, 283, 20, 2), (257, 250, 9, 1), (1031, 1001, 20, 2)])
+def test_lv_feature_branch_x3_matches_fp32_torch_form(R, U, k, s):
+    """The parity precisions' form (every product split-bf16, D and dP as hi / lo planes): within 3x the fp32 torch
+    form's error against float64 + 2e-5, at C and every variable's gradient"""
+    h0, ws, Lh = _lv_case(R, U, k, s, seed=R + U + 1)
+    dC = torch.randn(1, Lh, ws[0].shape[1], device=DEV, generator=torch.Generator(device=DEV).manual_seed(6))
+
+    def grads(fn):
+        for w in ws:
+            w.grad = None
+        C = fn()
+        (C * dC).sum().backward()
+        return C.detach(), [w.grad.detach().clone() for w in ws]
+
+    wd = [w.detach().double().requires_grad_(True) for w in ws]
+    C64 = _torch_form(h0.double(), wd, s, Lh, linear)
+    (C64 * dC.double()).sum().backward()
+    g64 = [w.grad for w in wd]
+    Ch, gh = grads(lambda: lv_feat_conv(h0, s, Lh, *ws, x3=True))
+    Cf, gf = grads(lambda: _torch_form(h0, ws, s, Lh, linear))
+    rel = lambda a, b: float((a.double() - b).norm() / (b.norm() + 1e-30))
+    eC_h, eC_f = rel(Ch, C64.detach()), rel(Cf, C64.detach())
+    assert eC_h < 3 * eC_f + 2e-5, (eC_h, eC_f)
+    for i, (a, b, ref) in enumerate(zip(gh, gf, g64)):
+        if i == 8:
+            assert float(a[:, 0, :].abs().max()) == 0.0
+        e_h, e_f = rel(a, ref), rel(b, ref)
+        assert e_h < 3 * e_f + 2e-5, (i, e_h, e_f)
+
+
+@pytest.mark.parametrize("R,U,k,s", [(301, 283, 20, 2), (257, 250, 9, 1), (1031, 1001, 20, 2)])
 def test_lv_feature_branch_matches_torch_form(R, U, k, s):
     h0, ws, Lh = _lv_case(R, U, k, s, seed=R + U)
     dC = torch.randn(1, Lh, ws[0].shape[1], device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))

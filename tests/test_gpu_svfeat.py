@@ -52,6 +52,35 @@ def test_gemm_x3_layouts(a_kmajor, b_kmajor, M, N, K):
         assert err < 3e-5, (split, err)
 
 
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(False, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(37, 45, 70), (300, 257, 96)])
+def test_gemm_x3_bf16_epilogues(a_kmajor, b_kmajor, M, N, K):
+    """x3 ELU / elu' epilogues: the output as a hi / lo plane pair (lo at C + M ldc), aux read the same way; the
+    pair's sum within 2^-15 of the float64 value (one bf16 plane alone is 2^-8)"""
+    from viforssms_amd import _lib
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + a_kmajor)
+    A, Ah, Al = _mat(K, M, _r8(M), g) if a_kmajor else _mat(M, K, _r8(K), g)
+    B, Bh, Bl = _mat(K, N, _r8(N), g) if b_kmajor else _mat(N, K, _r8(K), g)
+    Am = (A[:, :M].t() if a_kmajor else A[:, :K]).double()
+    Bm = (B[:, :N] if b_kmajor else B[:, :K].t()).double()
+    ref = Am @ Bm
+    ldc = _r8(N) + 8
+    Y = torch.full((2, M, ldc), float("nan"), device=DEV, dtype=torch.bfloat16)
+    gemm_bf16x3(M, N, K, Ah, Al, A.shape[1], a_kmajor, Bh, Bl, B.shape[1], b_kmajor, Y, ldc, _lib.GEMM_ELU_BF16)
+    torch.cuda.synchronize()
+    elu = torch.where(ref > 0, ref, torch.expm1(ref))
+    y = Y[0, :, :N].double() + Y[1, :, :N].double()
+    assert float((y - elu).abs().max()) <= 2 ** -15 * float(elu.abs().max())
+    assert torch.isnan(Y[:, :, N:].float()).all()
+    Z = torch.empty(2, M, ldc, device=DEV, dtype=torch.bfloat16)
+    gemm_bf16x3(M, N, K, Ah, Al, A.shape[1], a_kmajor, Bh, Bl, B.shape[1], b_kmajor, Z, ldc, _lib.GEMM_DELU_BF16,
+                aux=Y)
+    torch.cuda.synchronize()
+    dref = ref * torch.where(y < 0, y + 1, torch.ones_like(y))
+    z = Z[0, :, :N].double() + Z[1, :, :N].double()
+    assert float((z - dref).abs().max()) <= 2 ** -15 * float(dref.abs().max())
+
+
 def _sv_case(L, Cr, k, H=50, seed=0):
     g = torch.Generator(device=DEV).manual_seed(seed)
     r = lambda *sh, sc=1.0: (torch.randn(*sh, generator=g, device=DEV) * sc).requires_grad_(True)

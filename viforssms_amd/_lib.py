@@ -134,8 +134,8 @@ SIGNATURES = {
                                 _c_void_p, _c_void_p, _c_void_p]),
     "vissm_lv_mlp_bwd": (_i32, [ctypes.POINTER(LvFeatDesc), ctypes.POINTER(FeatParams), _c_void_p, _c_void_p,
                                 _c_void_p, _i32, ctypes.POINTER(FeatGrads), _c_void_p, _size_t, _c_void_p]),
-    "vissm_lv_pack": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _i32,
-                             _c_void_p, _c_void_p, _c_void_p]),
+    "vissm_lv_pack": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32,
+                             _i32, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_lv_conv_diag": (_i32, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vissm_lv_conv_diag_bwd": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                       _c_void_p, _c_void_p]),
@@ -144,7 +144,7 @@ SIGNATURES = {
     "vissm_gemm_bf16": (_i32, [ctypes.POINTER(GemmDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                _size_t, _c_void_p]),
     "vissm_gemm_bf16x3_workspace_size": (_size_t, [ctypes.POINTER(GemmDesc)]),
-    "vissm_gemm_bf16x3": (_i32, [ctypes.POINTER(GemmDesc)] + [_c_void_p] * 6 + [_size_t, _c_void_p]),
+    "vissm_gemm_bf16x3": (_i32, [ctypes.POINTER(GemmDesc)] + [_c_void_p] * 7 + [_size_t, _c_void_p]),
     "vissm_elbo_fwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vissm_elbo_bwd": (_i32, [ctypes.POINTER(ElboDesc), ctypes.POINTER(ElboData), _c_void_p, _c_void_p,

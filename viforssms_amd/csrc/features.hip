@@ -612,15 +612,17 @@ __global__ void lv_mlp_scatter_kernel(const float* __restrict__ red, int Cin, in
 // W3b [64][ldw] bf16: rows < H the time-mixing kernel W3 [H][U], row H its bias, the rest zero; Wc [R][ldc] bf16:
 // Wc[r][j H + h] = conv_w[j][1 + r][h] (the conv's feature channels), zero past k H
 __global__ void lv_pack_kernel(const float* __restrict__ w3, const float* __restrict__ b3, int H, int U, int ldw,
-                               __bf16* __restrict__ W3b, const float* __restrict__ cw, int R, int k, int ldc,
-                               __bf16* __restrict__ Wc, __bf16* __restrict__ Wc_lo) {
+                               __bf16* __restrict__ W3b, __bf16* __restrict__ W3b_lo, const float* __restrict__ cw,
+                               int R, int k, int ldc, __bf16* __restrict__ Wc, __bf16* __restrict__ Wc_lo) {
   const int64_t n1 = static_cast<int64_t>(kLvC) * ldw, n2 = static_cast<int64_t>(R) * ldc;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n1 + n2;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     if (i < n1) {
       const int c = static_cast<int>(i / ldw), u = static_cast<int>(i % ldw);
       const float v = u >= U ? 0.f : c < H ? w3[static_cast<int64_t>(c) * U + u] : c == H ? b3[u] : 0.f;
-      W3b[i] = static_cast<__bf16>(v);
+      const __bf16 hi = static_cast<__bf16>(v);
+      W3b[i] = hi;
+      if (W3b_lo) W3b_lo[i] = static_cast<__bf16>(v - static_cast<float>(hi));
     } else {
       const int64_t e = i - n1;
       const int r = static_cast<int>(e / ldc), n = static_cast<int>(e % ldc);
@@ -817,15 +819,15 @@ int vissm_lv_mlp_bwd(const VissmLvFeatDesc* d, const VissmFeatParams* w, const f
   return VISSM_OK;
 }
 
-int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, const float* conv_w, int R, int k,
-                  int ldc, void* Wc, void* Wc_lo, void* stream) {
+int vissm_lv_pack(const float* w3, const float* b3, int H, int U, int ldw, void* W3b, void* W3b_lo, const float* conv_w,
+                  int R, int k, int ldc, void* Wc, void* Wc_lo, void* stream) {
   VISSM_CHECK_ARG((ldw == 0 || (w3 && b3 && W3b && U >= 1 && ldw >= U)) && conv_w && Wc && H >= 1 && H < feat::kLvC &&
                       R >= 1 && k >= 1 && ldc >= k * H,
                   "lv_pack: bad argument");
   const int64_t n = static_cast<int64_t>(feat::kLvC) * ldw + static_cast<int64_t>(R) * ldc;
   hipLaunchKernelGGL(feat::lv_pack_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 16384))),
-                     dim3(256), 0, as_stream(stream), w3, b3, H, U, ldw, static_cast<__bf16*>(W3b), conv_w, R, k, ldc,
-                     static_cast<__bf16*>(Wc), static_cast<__bf16*>(Wc_lo));
+                     dim3(256), 0, as_stream(stream), w3, b3, H, U, ldw, static_cast<__bf16*>(W3b),
+                     static_cast<__bf16*>(W3b_lo), conv_w, R, k, ldc, static_cast<__bf16*>(Wc), static_cast<__bf16*>(Wc_lo));
   VISSM_CHECK_LAUNCH("lv_pack");
   return VISSM_OK;
 }

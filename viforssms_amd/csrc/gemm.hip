@@ -16,10 +16,11 @@
 // 8 banks mod 64).  Epilogues: fp32 store, ELU -> bf16, x elu'(y) of a bf16 ELU output -> bf16.  Split-K
 // (gridDim.z > 1) writes per-split fp32 partials that a fixed-order pass sums (deterministic).
 //
-// Split-bf16 form (vissm_gemm_bf16x3; SV's window-shared conv, SV_dense.py:56-62, at fp32-class accuracy): the K loop
-// runs over three passes of the K range, (A_hi, B_hi), (A_hi, B_lo), (A_lo, B_hi), into the same accumulators; each
-// pass is padded to a whole number of K steps, so a step never straddles two passes and split-K divides the 3 K
-// range like any other.
+// Split-bf16 form (vissm_gemm_bf16x3; SV's window-shared conv, SV_dense.py:56-62, and LV's branch at the parity
+// precisions, at fp32-class accuracy): the K loop runs over three passes of the K range, (A_hi, B_hi), (A_hi, B_lo),
+// (A_lo, B_hi), into the same accumulators; each pass is padded to a whole number of K steps, so a step never
+// straddles two passes and split-K divides the 3 K range like any other.  Its bf16 epilogues write the output as a
+// hi / lo plane pair (the lo plane M ldc elements after C) and read aux the same way.
 #include "common.hpp"
 
 namespace vissm {
@@ -262,28 +263,48 @@ __global__ __launch_bounds__(NT, VISSM_GEMM_MINB) void gemm_kernel(KArgs a, cons
         for (int e = 0; e < 8; ++e) x[e] = stg[rr * 68 + cc + e];
         __bf16* dst = reinterpret_cast<__bf16*>(Cv) + m * a.ldc + n;
         const bool full = n + 8 <= a.N && ((m * a.ldc + n) & 7) == 0;
-        bf8 o;
-        if constexpr (EPI == 1) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = static_cast<__bf16>(elu_acc(x[e]));
-        } else {
+        // X3: the output and aux are hi / lo plane pairs, the lo plane M ldc elements after the hi one
+        const int64_t plane = a.M * a.ldc;
+        auto ld8 = [&](const __bf16* src) {
           bf8 y;
-          const __bf16* src = aux + m * a.ldc + n;
           if (full) y = *reinterpret_cast<const bf8*>(src);
           else
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] = n + e < a.N ? src[e] : static_cast<__bf16>(0.f);
+          return y;
+        };
+        auto st8 = [&](__bf16* q, bf8 o) {
+          if (full) *reinterpret_cast<bf8*>(q) = o;
+          else
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (n + e < a.N) q[e] = o[e];
+        };
+        float v[8];
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = elu_acc(x[e]);
+        } else {
+          const __bf16* src = aux + m * a.ldc + n;
+          const bf8 y = ld8(src);
+          bf8 yl;
+          if constexpr (X3) yl = ld8(src + plane);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float yv = static_cast<float>(y[e]);
-            o[e] = static_cast<__bf16>(yv < 0.f ? x[e] * (yv + 1.f) : x[e]);
+            float yv = static_cast<float>(y[e]);
+            if constexpr (X3) yv += static_cast<float>(yl[e]);
+            v[e] = yv < 0.f ? x[e] * (yv + 1.f) : x[e];
           }
         }
-        if (full) *reinterpret_cast<bf8*>(dst) = o;
-        else
+        bf8 o;
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (n + e < a.N) dst[e] = o[e];
+        for (int e = 0; e < 8; ++e) o[e] = static_cast<__bf16>(v[e]);
+        st8(dst, o);
+        if constexpr (X3) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = static_cast<__bf16>(v[e] - static_cast<float>(o[e]));
+          st8(dst + plane, o);
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -334,7 +355,6 @@ static int gemm_launch(const VissmGemmDesc* d, const void* A, const void* A2, co
                   "%s: leading dimension below the row length", nm);
   VISSM_CHECK_ARG(d->ldc >= d->N, "%s: ldc < N", nm);
   VISSM_CHECK_ARG(d->epilogue >= VISSM_GEMM_F32 && d->epilogue <= VISSM_GEMM_DELU_BF16, "%s: epilogue", nm);
-  VISSM_CHECK_ARG(!x3 || d->epilogue == VISSM_GEMM_F32, "%s: the split-bf16 form has the fp32 epilogue only", nm);
   VISSM_CHECK_ARG(d->epilogue != VISSM_GEMM_DELU_BF16 || aux, "%s: the elu' epilogue needs aux", nm);
   const int split = d->split_k > 1 ? d->split_k : 1;
   VISSM_CHECK_ARG(split == 1 || (d->epilogue == VISSM_GEMM_F32 && d->ldc == d->N),
@@ -359,7 +379,9 @@ static int gemm_launch(const VissmGemmDesc* d, const void* A, const void* A2, co
   const __bf16* px = static_cast<const __bf16*>(aux);
 #define GEMM_EPI(AK, BKk)                                                                                      \
   do {                                                                                                       \
-    if (x3) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0, true>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    if (x3 && d->epilogue == VISSM_GEMM_F32) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0, true>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    else if (x3 && d->epilogue == VISSM_GEMM_ELU_BF16) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 1, true>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
+    else if (x3) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 2, true>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
     else if (d->epilogue == VISSM_GEMM_F32) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 0>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
     else if (d->epilogue == VISSM_GEMM_ELU_BF16) hipLaunchKernelGGL((gemm_kernel<AK, BKk, 1>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2); \
     else hipLaunchKernelGGL((gemm_kernel<AK, BKk, 2>), grid, dim3(NT), 0, st, a, pa, pb, out, px, pa2, pb2);   \
@@ -392,8 +414,8 @@ int vissm_gemm_bf16(const VissmGemmDesc* d, const void* A, const void* B, void* 
 size_t vissm_gemm_bf16x3_workspace_size(const VissmGemmDesc* d) { return vissm_gemm_workspace_size(d); }
 
 int vissm_gemm_bf16x3(const VissmGemmDesc* d, const void* A_hi, const void* A_lo, const void* B_hi, const void* B_lo,
-                      void* C, void* workspace, size_t ws_bytes, void* stream) {
-  return gemm_launch(d, A_hi, A_lo, B_hi, B_lo, C, nullptr, workspace, ws_bytes, stream, true);
+                      void* C, const void* aux, void* workspace, size_t ws_bytes, void* stream) {
+  return gemm_launch(d, A_hi, A_lo, B_hi, B_lo, C, aux, workspace, ws_bytes, stream, true);
 }
 
 }  // extern "C"

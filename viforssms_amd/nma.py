@@ -278,13 +278,16 @@ class IAF:
             return feat_conv(h0, s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"), p("feat1/bias"),
                              p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"), p("feat3/bias"),
                              p("conv/kernel"), p("conv/bias"))
-        # LV at the bf16 precision: the hand-written branch (ops.lv_feat_conv: vissm_lv_* + vissm_gemm_bf16), LV-cfg
-        # step 64.0 -> 62.1 ms against the torch form (profiles/r06/lvfeat/); VISSM_LV_FEAT=torch selects the latter
-        if f == "lv" and ts.is_cuda and gemm == "bf16" and os.environ.get("VISSM_LV_FEAT", "hip") != "torch":
+        # LV: the hand-written branch (ops.lv_feat_conv: vissm_lv_* + vissm_gemm_bf16) at the bf16 precision, LV-cfg
+        # step 64.0 -> 62.1 ms against the torch form (profiles/r06/lvfeat/; VISSM_LV_FEAT=torch selects the latter).
+        # At the parity precisions its split-bf16 form (vissm_gemm_bf16x3, hi / lo planes) measured 191.4 against the
+        # torch form's 190.5 ms per bf16x2f step (profiles/r06/lv_x3/), so there it runs on VISSM_LV_FEAT=hip only
+        lvf = os.environ.get("VISSM_LV_FEAT", "")
+        if f == "lv" and ts.is_cuda and ((gemm == "bf16" and lvf != "torch") or (gemm == "x3" and lvf == "hip")):
             p = self._p
             return lv_feat_conv(ts[:, :-1, :], s, Lh, p("feat0/kernel"), p("feat0/bias"), p("feat1/kernel"),
                                 p("feat1/bias"), p("feat2/kernel"), p("feat2/bias"), p("feat3/kernel"),
-                                p("feat3/bias"), p("conv/kernel"), p("conv/bias"))
+                                p("feat3/bias"), p("conv/kernel"), p("conv/bias"), x3=gemm == "x3")
         # SV (k = 50) at the non-fp32 precisions: the hand-written branch (ops.sv_feat_conv: vissm_lv_mlp_* with the
         # first-difference input, the conv as one split-bf16 matrix-core GEMM each way); VISSM_SV_FEAT=torch selects
         # the torch form (fp32 layers, linear_x3 conv)

@@ -294,15 +294,16 @@ def gemm_bf16(M: int, N: int, K: int, A, lda: int, a_kmajor: bool, B, ldb: int, 
 
 
 def gemm_bf16x3(M: int, N: int, K: int, A, A_lo, lda: int, a_kmajor: bool, B, B_lo, ldb: int, b_kmajor: bool, C,
-                ldc: int, split_k: int = 1):
-    """C = A_hi B_hi + A_hi B_lo + A_lo B_hi (fp32 C): the split-bf16 form of gemm_bf16, fp32-class products"""
+                ldc: int, epilogue: int = 0, aux=None, split_k: int = 1):
+    """C = A_hi B_hi + A_hi B_lo + A_lo B_hi: the split-bf16 form of gemm_bf16, fp32-class products (fp32 C, or for
+    the ELU / elu' epilogues a [2][M][ldc] bf16 hi / lo plane pair, aux the same)"""
     lib = _lib.load()
-    d = _lib.GemmDesc(M, N, K, lda, ldb, ldc, int(a_kmajor), int(b_kmajor), _lib.GEMM_F32, split_k)
+    d = _lib.GemmDesc(M, N, K, lda, ldb, ldc, int(a_kmajor), int(b_kmajor), epilogue, split_k)
     nb = lib.vissm_gemm_bf16x3_workspace_size(ctypes.byref(d))
     ws = _workspace(nb, C.device) if nb else None
     check(lib.vissm_gemm_bf16x3(ctypes.byref(d), ptr(A), ptr(A_lo), ptr(B), ptr(B_lo), ptr(C),
-                                ptr(ws) if ws is not None else None, nb, _lib.stream_handle(C.device)),
-          "vissm_gemm_bf16x3")
+                                ptr(aux) if aux is not None else None, ptr(ws) if ws is not None else None, nb,
+                                _lib.stream_handle(C.device)), "vissm_gemm_bf16x3")
 
 
 def _r8(n: int) -> int:
@@ -312,15 +313,25 @@ def _r8(n: int) -> int:
 class LvFeatConvFn(torch.autograd.Function):
     """Lotka-Volterra's window-shared conv input C [n_win, Lh, H] (lotka_volterra_partial.py:71-82): the three dense +
     ELU layers of the window's time features h0 [n_win, R, Cin] (fp32, vissm_lv_mlp_*), the time-mixing layer
-    D = elu(H3 W3 + b3) [R, U] and the conv over D's R channels (transposed by the reference, U its time axis) as bf16
+    D = elu(H3 W3 + b3) [R, U] and the conv over D's R channels (transposed by the reference, U its time axis) as
     matrix-core GEMMs (vissm_gemm_bf16: the layer with its ELU in the epilogue, then G = D^T Wc [U, k H] and the
     conv's diagonal sum), and the backward the same way (dD with elu' in the epilogue, dWc = D dG, dW3 = H3^T dP and
-    dH3 = dP W3^T split over K).  The bf16 precision's arithmetic (the torch form: fp32 layers, linear_bf16 conv)
-    plus bf16 operands in the time-mixing layer; the gradient reaches the four dense layers and the conv kernel (its
-    sample channel 0 gets zero: the flow kernel's w_eps) and bias."""
+    dH3 = dP W3^T split over K).  x3 = False: the bf16 precision's arithmetic (the torch form: fp32 layers,
+    linear_bf16 conv) plus bf16 operands in the time-mixing layer.  x3 = True (the parity precisions): every product
+    in the split-bf16 form (vissm_gemm_bf16x3, fp32-class; D and dP kept as hi / lo plane pairs).  The gradient
+    reaches the four dense layers and the conv kernel (its sample channel 0 gets zero: the flow kernel's w_eps) and
+    bias."""
 
     @staticmethod
-    def forward(ctx, h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
+    def _mm(x3, M, N, K, A, lda, akm, B, ldb, bkm, C, ldc, epi=0, aux=None, split=1):
+        """C = A B with A / B (hi, lo) pairs: one bf16 product (x3 False: the hi planes) or the split-bf16 form"""
+        if x3:
+            gemm_bf16x3(M, N, K, A[0], A[1], lda, akm, B[0], B[1], ldb, bkm, C, ldc, epi, aux, split)
+        else:
+            gemm_bf16(M, N, K, A[0], lda, akm, B[0], ldb, bkm, C, ldc, epi, aux, split)
+
+    @staticmethod
+    def forward(ctx, h0, s, Lh, x3, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
         ws = (W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
         _require_gpu(*ws)
         n_win, R, Cin = h0.shape
@@ -333,51 +344,55 @@ class LvFeatConvFn(torch.autograd.Function):
                                   "do not match")
         dev = h0.device
         Up, NC = _r8(U), _r8(k * H)
+        npl = 2 if x3 else 1   # bf16 planes per operand
         lib, st = _lib.load(), _lib.stream_handle(dev)
         d = _lib.LvFeatDesc(n_win, R, Cin, H, h0.stride(0) if n_win > 1 else R * Cin, 3, 0)
         p = _feat_params(ws)
         act = torch.empty(3, n_win, R, H, dtype=torch.float32, device=dev)
-        H3b = torch.empty(n_win, R, 64, dtype=torch.bfloat16, device=dev)
-        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(act), ptr(H3b), None, st),
-              "vissm_lv_mlp_fwd")
-        W3b = torch.empty(64, Up, dtype=torch.bfloat16, device=dev)
-        Wc = torch.empty(R, NC, dtype=torch.bfloat16, device=dev)
-        check(lib.vissm_lv_pack(ptr(W3), ptr(b3), H, U, Up, ptr(W3b), ptr(conv_w), R, k, NC, ptr(Wc), None, st),
-              "vissm_lv_pack")
-        D = torch.empty(n_win, R, Up, dtype=torch.bfloat16, device=dev)
+        H3b = torch.empty(npl, n_win, R, 64, dtype=torch.bfloat16, device=dev)
+        check(lib.vissm_lv_mlp_fwd(ctypes.byref(d), ctypes.byref(p), ptr(h0), ptr(act), ptr(H3b[0]),
+                                   ptr(H3b[1]) if x3 else None, st), "vissm_lv_mlp_fwd")
+        W3b = torch.empty(npl, 64, Up, dtype=torch.bfloat16, device=dev)
+        Wc = torch.empty(npl, R, NC, dtype=torch.bfloat16, device=dev)
+        check(lib.vissm_lv_pack(ptr(W3), ptr(b3), H, U, Up, ptr(W3b[0]), ptr(W3b[1]) if x3 else None, ptr(conv_w), R,
+                                k, NC, ptr(Wc[0]), ptr(Wc[1]) if x3 else None, st), "vissm_lv_pack")
+        D = torch.empty(n_win, npl, R, Up, dtype=torch.bfloat16, device=dev)   # hi (/ lo) planes per window
         G = torch.empty(U, NC, dtype=torch.float32, device=dev)
         C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=dev)
         sk = int(os.environ.get("VISSM_LV_SPLIT", "5"))
+        mm = LvFeatConvFn._mm
         for w in range(n_win):
-            gemm_bf16(R, U, 64, H3b[w], 64, False, W3b, Up, True, D[w], Up, _lib.GEMM_ELU_BF16)
-            gemm_bf16(U, NC, R, D[w], Up, True, Wc, NC, True, G, NC, _lib.GEMM_F32, split_k=sk)
+            mm(x3, R, U, 64, H3b[:, w], 64, False, W3b, Up, True, D[w], Up, _lib.GEMM_ELU_BF16)
+            mm(x3, U, NC, R, D[w], Up, True, Wc, NC, True, G, NC, split=sk)
             check(lib.vissm_lv_conv_diag(ptr(G), NC, ptr(conv_b), H, k, s, Lh, ptr(C[w]), st), "vissm_lv_conv_diag")
         ctx.save_for_backward(h0, act, H3b, D, W3b, Wc, *ws)
-        ctx.dims = (d, n_win, R, H, U, k, s, Lh, Up, NC)
+        ctx.dims = (d, n_win, R, H, U, k, s, Lh, Up, NC, x3)
         return C
 
     @staticmethod
     def backward(ctx, dC):
         h0, act, H3b, D, W3b, Wc, *ws = ctx.saved_tensors
-        d, n_win, R, H, U, k, s, Lh, Up, NC = ctx.dims
+        d, n_win, R, H, U, k, s, Lh, Up, NC, x3 = ctx.dims
         dev = dC.device
         dC = dC.contiguous()
+        npl = 2 if x3 else 1
         lib, st = _lib.load(), _lib.stream_handle(dev)
-        dG = torch.empty(U, NC, dtype=torch.bfloat16, device=dev)
-        dP = torch.empty(R, Up, dtype=torch.bfloat16, device=dev)
+        dG = torch.empty(npl, U, NC, dtype=torch.bfloat16, device=dev)
+        dP = torch.empty(npl, R, Up, dtype=torch.bfloat16, device=dev)
         dWc = torch.empty(n_win, R, NC, dtype=torch.float32, device=dev)
         dW3b = torch.empty(n_win, 64, U, dtype=torch.float32, device=dev)
         dH3 = torch.empty(n_win, R, 64, dtype=torch.float32, device=dev)
         dcb = torch.empty(n_win, H, dtype=torch.float32, device=dev)
+        sk = int(os.environ.get("VISSM_LV_SPLIT", "5"))
+        sw = int(os.environ.get("VISSM_LV_SPLIT_W3", "8"))
+        mm = LvFeatConvFn._mm
         for w in range(n_win):
-            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG), None, ptr(dcb[w]), st),
-                  "vissm_lv_conv_diag_bwd")
-            gemm_bf16(R, U, NC, Wc, NC, False, dG, NC, False, dP, Up, _lib.GEMM_DELU_BF16, aux=D[w])
-            gemm_bf16(R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, _lib.GEMM_F32,
-                      split_k=int(os.environ.get("VISSM_LV_SPLIT", "5")))
-            sw = int(os.environ.get("VISSM_LV_SPLIT_W3", "8"))
-            gemm_bf16(64, U, R, H3b[w], 64, True, dP, Up, True, dW3b[w], U, _lib.GEMM_F32, split_k=sw)
-            gemm_bf16(R, 64, U, dP, Up, False, W3b, Up, False, dH3[w], 64, _lib.GEMM_F32, split_k=sw)
+            check(lib.vissm_lv_conv_diag_bwd(ptr(dC[w]), H, k, s, Lh, U, NC, ptr(dG[0]), ptr(dG[1]) if x3 else None,
+                                             ptr(dcb[w]), st), "vissm_lv_conv_diag_bwd")
+            mm(x3, R, U, NC, Wc, NC, False, dG, NC, False, dP, Up, _lib.GEMM_DELU_BF16, aux=D[w])
+            mm(x3, R, NC, U, D[w], Up, False, dG, NC, True, dWc[w], NC, split=sk)
+            mm(x3, 64, U, R, H3b[:, w], 64, True, dP, Up, True, dW3b[w], U, split=sw)
+            mm(x3, R, 64, U, dP, Up, False, W3b, Up, False, dH3[w], 64, split=sw)
         if n_win > 1:   # (the reference's LV windows: one per step at the benchmark shapes)
             dWc, dW3b, dcb = dWc.sum(0, keepdim=True), dW3b.sum(0, keepdim=True), dcb.sum(0, keepdim=True)
         gr = [torch.empty_like(t) for t in ws[:6]]
@@ -391,11 +406,11 @@ class LvFeatConvFn(torch.autograd.Function):
         wsb = _workspace(nb, dev)
         check(lib.vissm_lv_mlp_bwd(ctypes.byref(d), ctypes.byref(_feat_params(ws)), ptr(h0), ptr(act), ptr(dH3), 64,
                                    ctypes.byref(g), ptr(wsb), nb, st), "vissm_lv_mlp_bwd")
-        return (None, None, None, *gr, dW3b[0, :H], dW3b[0, H], dconv_w, dcb[0])
+        return (None, None, None, None, *gr, dW3b[0, :H], dW3b[0, H], dconv_w, dcb[0])
 
 
-def lv_feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b):
-    return LvFeatConvFn.apply(h0, s, Lh, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
+def lv_feat_conv(h0, s: int, Lh: int, W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b, x3: bool = False):
+    return LvFeatConvFn.apply(h0, s, Lh, bool(x3), W0, b0, W1, b1, W2, b2, W3, b3, conv_w, conv_b)
 
 
 class SvFeatConvFn(torch.autograd.Function):
@@ -432,7 +447,7 @@ class SvFeatConvFn(torch.autograd.Function):
                                    ptr(Fl), st), "vissm_lv_mlp_fwd")
         Wch = torch.empty(H, NCp, dtype=torch.bfloat16, device=dev)
         Wcl = torch.empty_like(Wch)
-        check(lib.vissm_lv_pack(None, None, H, 0, 0, None, ptr(conv_w), H, k, NCp, ptr(Wch), ptr(Wcl), st),
+        check(lib.vissm_lv_pack(None, None, H, 0, 0, None, None, ptr(conv_w), H, k, NCp, ptr(Wch), ptr(Wcl), st),
               "vissm_lv_pack")
         G = torch.empty(R, NCp, dtype=torch.float32, device=dev)
         C = torch.empty(n_win, Lh, H, dtype=torch.float32, device=dev)
