@@ -108,7 +108,9 @@ class ParamStore:
         for name, t in self.tensors.items():
             a, sz = self.offsets[name]
             g = t.grad
-            if g is not None and g.data_ptr() != self.grad[a:a + sz].data_ptr():
+            if g is None:   # no gradient reached it (released view): its flat slice is still zero_grad's zeros
+                t.grad = self.grad[a:a + sz].view(t.shape)
+            elif g.data_ptr() != self.grad[a:a + sz].data_ptr():
                 v = self.grad[a:a + sz].view(t.shape)
                 dst.append(v)
                 src.append(g)
